@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: images/sec of MultiPersonKeypointModel.forward (eval, given boxes)
+on the BASELINE.json headline config C2 -- batch 64 per GPU, synthetic
+256x192x3 images, 1 person box per image, 17 COCO keypoints, heatmap head +
+soft-argmax decode -- through the native HIP path.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One process per GPU; images shard across ranks (weak scaling, B per rank) and
+each step all-gathers the per-image keypoints/visibilities to every rank over
+RCCL (result collation, BASELINE C4).  Rank 0 prints one JSON line with the
+whole-job rate, the dominant kernel's roofline fraction (HIP events on the
+launch stream, inside the timed region) and the CPU-oracle baseline timed on
+this host (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (str(ROOT), str(ROOT / "keypoint-detection_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def conv_flops(cin, cout, k, h, w, groups=1):
+    return 2.0 * cout * (cin // groups) * k * k * h * w
+
+
+def flops_per_image(H, W, P, in_ch=3):
+    """Algorithmic FLOPs (2*MAC of conv/linear, BN folded, dead FPN levels 1-3
+    excluded) -- SURVEY.md §8(d)."""
+    from oracle.kpd_oracle import MBV3_SMALL_BNECK, make_divisible
+    h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    f = conv_flops(in_ch, 16, 3, h, w)
+    sizes = [(h, w)]
+    for cin, k, exp, cout, se, _a, s in MBV3_SMALL_BNECK:
+        if exp != cin:
+            f += conv_flops(cin, exp, 1, h, w)
+        ho, wo = (h + 2 * ((k - 1) // 2) - k) // s + 1, (w + 2 * ((k - 1) // 2) - k) // s + 1
+        f += conv_flops(exp, exp, k, ho, wo, groups=exp)
+        if se:
+            sq = make_divisible(exp // 4, 8)
+            f += 2.0 * (exp * sq * 2)
+        f += conv_flops(exp, cout, 1, ho, wo)
+        h, w = ho, wo
+        sizes.append((h, w))
+    f += conv_flops(96, 576, 1, h, w)
+    taps = [sizes[0], sizes[3], sizes[8], sizes[11]]
+    for cin, (th, tw) in zip((16, 24, 48, 576), taps):
+        f += conv_flops(cin, 128, 1, th, tw)
+    fpn0 = conv_flops(128, 128, 3, *sizes[0])
+    f += fpn0 + 2.0 * (128 * 8 * 2) * 2
+    hm_convs = [conv_flops(64, 256, 3, 56, 56), conv_flops(256, 256, 3, 56, 56), conv_flops(256, 64, 3, 56, 56)]
+    head = sum(hm_convs) + conv_flops(64, 17, 1, 56, 56) + conv_flops(2, 1, 7, 56, 56) + 2.0 * (64 * 4 * 2) * 2
+    return {"total": f + P * head, "fpn0": fpn0, "hm_conv1": hm_convs[0] * P, "hm_conv2": hm_convs[1] * P,
+            "hm_conv3": hm_convs[2] * P}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=192)
+    ap.add_argument("--persons", type=int, default=1)
+    ap.add_argument("--precision", default="mixed", choices=["fp32", "mixed"])
+    ap.add_argument("--cpu-sample", type=int, default=8, help="images in the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc_fpn0.json"),
+                    help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
+    return ap.parse_args()
+
+
+def cpu_baseline(sd, img, boxes, seconds, threads):
+    """The oracle (a plain-torch restatement of the reference forward, same
+    per-box loop) timed on this host's cores."""
+    from oracle import kpd_oracle as O
+    torch.set_num_threads(threads)
+    batch = {"image": img, "bboxes": boxes}
+    out = O.forward(sd, batch)        # warmup + outputs for parity
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        O.forward(sd, batch)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or runs >= 50:
+            break
+    return out, img.shape[0] * runs / el, runs
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=dev)
+
+    from dll import _native
+    from dll.configs import ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+
+    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=a.precision)
+    sd = synthetic_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(dev).eval()
+    B, P = a.batch, a.persons
+    img_cpu = synthetic_images(B, 3, a.height, a.width, seed=1234 + 7919 * rank)
+    box_cpu = synthetic_boxes(B, P, seed=1235 + 7919 * rank)
+    img, boxes = img_cpu.to(dev), box_cpu.to(dev)
+    batch = {"image": img, "bboxes": boxes}
+    plan = m.native_plan(dev)
+
+    gather_bufs = None
+    if dist and not a.no_gather:
+        import torch.distributed as tdist
+        gather_bufs = ([torch.empty(B, P, 1, 17, 2, device=dev) for _ in range(world)],
+                       [torch.empty(B, P, 1, 17, 3, device=dev) for _ in range(world)])
+
+    def step():
+        out = m(batch)
+        if gather_bufs is not None:
+            tdist.all_gather(gather_bufs[0], out["keypoints"])
+            tdist.all_gather(gather_bufs[1], out["visibilities"])
+        return out
+
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            out = step()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        plan.timing(True)
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        el = time.perf_counter() - t0
+        plan.timing(False)
+    el_t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if dist:
+        tdist.all_reduce(el_t, op=tdist.ReduceOp.MAX)
+    el = float(el_t.item())
+
+    stages = {}
+    for s in _native.STAGES:
+        ms, n = plan.timing_query(s)
+        if n:
+            stages[s] = ms / n
+    fl = flops_per_image(a.height, a.width, P)
+    mfma = {"fpn0": ("fp32", fl["fpn0"] * B)}
+    hdt = "bf16" if a.precision == "mixed" else "fp32"
+    for s in ("hm_conv1", "hm_conv2", "hm_conv3"):
+        mfma[s] = (hdt, fl[s] * B)
+    dom = max(stages, key=lambda k: stages[k]) if stages else None
+    roof = None
+    if dom in mfma:
+        dt, flop = mfma[dom]
+        ach = flop / (stages[dom] * 1e-3) / 1e12
+        traffic = None
+        pj = Path(a.pmc_json)
+        if pj.exists():
+            try:
+                traffic = json.loads(pj.read_text()).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "mfma", "kernel": f"{dom} ({dt} MFMA implicit-GEMM conv)", "achieved": round(ach, 2),
+                "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dt], 4),
+                "traffic": traffic, "flop_per_launch": flop, "avg_ms": round(stages[dom], 4)}
+
+    total_imgs = B * world * a.steps
+    line = {
+        "metric": "images/sec @ 256x192 COCO-17 (MultiPersonKeypointModel.forward, given boxes)",
+        "value": round(total_imgs / el, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16+fp32" if a.precision == "mixed" else "fp32",
+        "data": "synthetic (seeded U[0,1) images ImageNet-normalised, seeded boxes, seed-0 random weights)",
+        "config": {"workload": "C2: batch 64/GPU, 256x192x3, 1 box/img, heatmap head + soft-argmax decode",
+                   "model": "MultiPersonKeypointModel (MobileNetV3-Small+FPN, HeatmapHead)",
+                   "global_batch": B * world, "height": a.height, "width": a.width, "persons": P,
+                   "precision": a.precision, "parallelism": f"dp{world}",
+                   "gather": bool(gather_bufs is not None)},
+        "gflop_per_image": round(fl["total"] / 1e9, 3),
+        "achieved_tflops_total": round(fl["total"] * total_imgs / el / 1e12, 2),
+        "roofline": roof,
+        "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        S = min(a.cpu_sample, B)
+        ref, cpu_rate, runs = cpu_baseline(sd, img_cpu[:S], box_cpu[:S], a.cpu_seconds, threads)
+        line["cpu_baseline"] = {"value": round(cpu_rate, 3), "unit": "images/s", "cores": threads, "kind": "port",
+                                "sample": f"{S} images x {runs} runs of the same workload (oracle/kpd_oracle.py "
+                                          f"forward, per-box loop as the reference)"}
+        line["gpu_vs_cpu"] = round(line["value"] / cpu_rate, 1)
+        gk = out["keypoints"][:S].cpu()
+        d = (gk - ref["keypoints"]).norm(dim=-1)
+        line["parity"] = {"pck@0.5": float((d <= 0.5).float().mean()), "pck@0.002": float((d <= 0.002).float().mean()),
+                          "max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
+                          "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
+                          "images": S}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+/* kpd.h -- C ABI of the MI355X-native keypoint-detection hot path (libkpd.so).
+ *
+ * Drop-in boundary for the reference's `MultiPersonKeypointModel.forward`
+ * (eval, caller-given person boxes).  Plain pointers and sizes only; device
+ * pointers are HIP device memory on the plan's device, streams are
+ * hipStream_t passed as void*.  The library owns the plan (packed weights,
+ * workspace); the caller owns every input/output buffer.
+ *
+ * Reference interfaces replaced (paths under the reference repo):
+ *   kpd_plan_create/set_tensor/finalize
+ *       <- MultiPersonKeypointModel.__init__ + load_state_dict
+ *          dll/models/keypoint_model.py:49-71, scripts/predict.py:30-62
+ *          (tensor names are the reference's state-dict keys; BN folding and
+ *           NHWC/MFMA repacking happen inside finalize)
+ *   kpd_forward
+ *       <- MultiPersonKeypointModel.forward(batch) with batch['bboxes']
+ *          dll/models/keypoint_model.py:73-210 (eval / no_grad branch):
+ *          backbone.py:258-264, keypoint_model.py:653-661, :212-228,
+ *          heatmap_head.py:81-113, keypoint_model.py:250-313, :230-248
+ *   kpd_nms
+ *       <- PERSON_HEAD.non_max_suppression  dll/models/person_head.py:96-139
+ *
+ * Every function returns 0 on success or a negative KPD_E* code; the message
+ * of the last failure on the calling thread is available from kpd_last_error().
+ */
+#ifndef KPD_H_
+#define KPD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KPD_OK 0
+#define KPD_EINVAL (-1)     /* bad argument / shape (reference raises ValueError) */
+#define KPD_EHIP (-2)       /* HIP runtime error */
+#define KPD_ESTATE (-3)     /* plan not finalized / missing weights */
+
+#define KPD_PRECISION_FP32 0   /* every conv on fp32-input MFMA (exact fp32 products) */
+#define KPD_PRECISION_MIXED 1  /* heatmap-head convs on bf16 MFMA, fp32 accumulate; backbone fp32 */
+
+typedef struct kpd_plan kpd_plan;
+
+const char* kpd_last_error(void);
+const char* kpd_version(void);
+
+/* Create an empty plan bound to HIP device `device`.  in_channels: 1 or 3
+ * (BackboneConfig.in_channels, reference backbone.py:251-252). */
+int kpd_plan_create(int device, int in_channels, kpd_plan** out);
+
+/* Register one reference state-dict tensor (fp32, host memory, contiguous,
+ * shape as in the reference).  Unknown names are ignored (the reference's
+ * predict.py filters unknown keys the same way, predict.py:47-57). */
+int kpd_plan_set_tensor(kpd_plan* plan, const char* name, const float* host_data,
+                        const int64_t* shape, int ndim);
+
+/* Fold BN, repack weights (NHWC / MFMA layouts) and upload them.
+ * Fails with KPD_ESTATE listing any missing tensor. */
+int kpd_plan_finalize(kpd_plan* plan, int precision);
+
+void kpd_plan_destroy(kpd_plan* plan);
+
+/* Full eval forward with given boxes.
+ *   image:  [B][C][H][W] fp32 (NCHW, as the reference receives it), device
+ *   boxes:  [nbox_images][P][4] fp32 cxcywh normalised to [0,1], device;
+ *           nbox_images <= B (the reference iterates over the box list)
+ *   keypoints:    [nbox_images][P][1][17][2]  fp32 out
+ *   visibilities: [nbox_images][P][1][17][3]  fp32 out (one-hot 3-class)
+ *   heatmap:      [nbox_images][P][17][56][56] fp32 out, may be NULL
+ *   topk_out:     [B][64] int32 channel indices, may be NULL (debug)
+ * All-zero boxes are skipped and the remaining persons compacted, images
+ * without a valid box get the reference's dummy person, P is kept as the
+ * padded person count -- exactly keypoint_model.py:138-206. */
+int kpd_forward(kpd_plan* plan, const float* image, int B, int C, int H, int W,
+                const float* boxes, int nbox_images, int P,
+                float* keypoints, float* visibilities, float* heatmap,
+                int32_t* topk_out, void* stream);
+
+/* Copy an internal buffer recorded by the last kpd_forward into `dst`
+ * (device memory, `bytes` long).  Names: "feat0" ([B][Hf][Wf][128] NHWC f32),
+ * "scores" ([B][128] f32), "roi" ([R][56][56][64] f32), "tap0".."tap3".
+ * Writes the buffer size to *size_out when dst == NULL. */
+int kpd_debug_copy(kpd_plan* plan, const char* name, void* dst, size_t bytes, size_t* size_out,
+                   void* stream);
+
+/* Per-stage device timing with HIP events recorded on the launch stream.
+ * kpd_plan_timing(plan, 1) clears previous records and enables recording for
+ * subsequent kpd_forward calls; kpd_plan_timing_query returns the summed
+ * milliseconds and the number of recorded launches of one stage
+ * ("body", "fpn_lateral", "fpn0", "topk", "roi_align", "hm_attention",
+ * "hm_conv1", "hm_conv2", "hm_conv3", "hm_final_decode"). */
+int kpd_plan_timing(kpd_plan* plan, int enable);
+int kpd_plan_timing_query(kpd_plan* plan, const char* stage, double* total_ms, int* count);
+
+/* Greedy NMS on one set of n cxcywh boxes (device), reference semantics
+ * (IoU > thr suppressed, score-descending order, ties -> lower index).
+ * keep: [n] int32 out (first *n_keep valid), n_keep: [1] int32 out (device).
+ * max_output <= 0 means unlimited. */
+int kpd_nms(const float* boxes, const float* scores, int n, float iou_threshold, int max_output,
+            int32_t* keep, int32_t* n_keep, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KPD_H_ */

@@ -1,0 +1,370 @@
+// Channel attention + top-k, batched ROI-align, HeatmapHead attention, final
+// 1x1 + sigmoid, and fused soft-argmax / visibility / coordinate decode (gfx950).
+//
+// Reference (file:line under /root/reference):
+//   ChannelAttention + select_top_k_channels  dll/models/keypoint_model.py:18-44,653-661
+//   extract_roi_features / box corners        dll/models/keypoint_model.py:212-228,630-638
+//   torchvision roi_align (aligned=False, sampling_ratio=-1), restated
+//   HeatmapHead channel/spatial attention     dll/models/heatmap_head.py:94-102,115-151
+//   final 1x1 + sigmoid                       dll/models/heatmap_head.py:40-44,111
+//   decode_heatmap / _soft_argmax             dll/models/keypoint_model.py:250-313
+//   convert_to_original_coords                dll/models/keypoint_model.py:230-248
+//   zero-box skip / dummy / padding rules     dll/models/keypoint_model.py:149-199,640-651
+//
+// All ROIs of a batch are processed together as one [R,56,56,C] NHWC tensor
+// (R = B*P); the reference's per-box Python loop becomes grid dimensions.
+#include "kpd_common.h"
+#include "kpd_kernels.h"
+
+namespace {
+constexpr int HM = 56;              // ROI / heatmap side
+constexpr int HMP = HM * HM;        // 3136
+constexpr int NK = 17;              // keypoints
+constexpr int TOPK = 64;
+constexpr int FC = 128;             // FPN channels
+
+// ---------------------------------------------------------------- top-k
+// One 128-thread workgroup per image.  stats: [N][tiles][2][128].
+__global__ __launch_bounds__(128) void topk_kernel(const float* __restrict__ stats, int tiles, int HW,
+                                                   const float* __restrict__ w0, const float* __restrict__ b0,
+                                                   const float* __restrict__ w2, const float* __restrict__ b2,
+                                                   int32_t* __restrict__ topk, float* __restrict__ scores_out) {
+  __shared__ float avg[FC], mx[FC], h[16], sc[FC];
+  const int n = blockIdx.x, c = threadIdx.x;
+  const float* st = stats + (size_t)n * tiles * 2 * FC;
+  float s = 0.f, m = -INFINITY;
+  for (int t = 0; t < tiles; ++t) {
+    s += st[t * 2 * FC + c];
+    m = fmaxf(m, st[t * 2 * FC + FC + c]);
+  }
+  avg[c] = s / (float)HW;
+  mx[c] = m;
+  __syncthreads();
+  if (c < 16) {  // hidden units: 0..7 for avg branch, 8..15 for max branch
+    const int j = c & 7;
+    const float* v = (c < 8) ? avg : mx;
+    float a = b0[j];
+    for (int k = 0; k < FC; ++k) a = fmaf(w0[j * FC + k], v[k], a);
+    h[c] = fmaxf(a, 0.f);
+  }
+  __syncthreads();
+  float oa = b2[c], om = b2[c];
+  for (int j = 0; j < 8; ++j) {
+    oa = fmaf(w2[c * 8 + j], h[j], oa);
+    om = fmaf(w2[c * 8 + j], h[8 + j], om);
+  }
+  const float score = kpd_sigmoid(oa + om);
+  sc[c] = score;
+  __syncthreads();
+  // rank = number of channels ordered before c (score desc, index asc on ties)
+  int rank = 0;
+  for (int k = 0; k < FC; ++k) {
+    const float o = sc[k];
+    rank += (o > score) || (o == score && k < c);
+  }
+  if (rank < TOPK) topk[n * TOPK + rank] = c;
+  if (scores_out) scores_out[n * FC + c] = score;
+}
+
+// ---------------------------------------------------------------- slot map
+// One thread per image: compaction of non-zero boxes (keypoint_model.py:149-153),
+// and the "no valid person" dummy (vis class 0 = 1, :171-179).
+__global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, int32_t* __restrict__ slot,
+                               float* __restrict__ vis_out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int cnt = 0;
+  for (int p = 0; p < P; ++p) {
+    const float* bx = boxes + ((size_t)b * P + p) * 4;
+    const bool zero = bx[0] == 0.f && bx[1] == 0.f && bx[2] == 0.f && bx[3] == 0.f;
+    slot[b * P + p] = zero ? -1 : cnt++;
+  }
+  if (cnt == 0 && P > 0)
+    for (int k = 0; k < NK; ++k) vis_out[((size_t)b * P * NK + k) * 3 + 0] = 1.f;
+}
+
+// ---------------------------------------------------------------- ROI align
+// grid (56 output rows, R); 256 threads = 4 waves; lane = selected channel.
+// feat: FPN level-0 NHWC [B][Hf][Wf][Cf]; channel gather through topk (the
+// reference materialises features[b, topk] first -- here it is an index).
+// Also emits per-(roi,row) channel sum/max partials for HeatmapHead attention.
+__global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
+                                                        const int32_t* __restrict__ topk,
+                                                        const float* __restrict__ boxes, int P,
+                                                        float* __restrict__ roi, float* __restrict__ roi_stats) {
+  __shared__ float red[4][2][TOPK];
+  const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* bx = boxes + (size_t)r * 4;
+  const float cx = bx[0], cy = bx[1], bw = bx[2], bh = bx[3];
+  const float x1 = fminf(fmaxf(cx - bw / 2.f, 0.f), 1.f) * (float)Wf;
+  const float y1 = fminf(fmaxf(cy - bh / 2.f, 0.f), 1.f) * (float)Hf;
+  const float x2 = fminf(fmaxf(cx + bw / 2.f, 0.f), 1.f) * (float)Wf;
+  const float y2 = fminf(fmaxf(cy + bh / 2.f, 0.f), 1.f) * (float)Hf;
+  const float roi_w = fmaxf(x2 - x1, 1.f), roi_h = fmaxf(y2 - y1, 1.f);
+  const float bin_w = roi_w / (float)HM, bin_h = roi_h / (float)HM;
+  const int gw = (int)ceilf(roi_w / (float)HM), gh = (int)ceilf(roi_h / (float)HM);
+  const float count = (float)max(gw * gh, 1);
+  const int ch = topk[b * TOPK + lane];
+  const float* fb = feat + (size_t)b * Hf * Wf * Cf + ch;
+
+  float s_sum = 0.f, s_max = -INFINITY;
+  for (int pw = wave; pw < HM; pw += 4) {
+    float acc = 0.f;
+    for (int iy = 0; iy < gh; ++iy) {
+      float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
+      for (int ix = 0; ix < gw; ++ix) {
+        float x = x1 + (float)pw * bin_w + ((float)ix + 0.5f) * bin_w / (float)gw;
+        if (y < -1.f || y > (float)Hf || x < -1.f || x > (float)Wf) continue;
+        float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
+        int yl = (int)yy, xl = (int)xx, yh, xh;
+        if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
+        if (xl >= Wf - 1) { xh = xl = Wf - 1; xx = (float)xl; } else xh = xl + 1;
+        const float ly = yy - (float)yl, lx = xx - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
+        const float v1 = fb[((size_t)yl * Wf + xl) * Cf], v2 = fb[((size_t)yl * Wf + xh) * Cf];
+        const float v3 = fb[((size_t)yh * Wf + xl) * Cf], v4 = fb[((size_t)yh * Wf + xh) * Cf];
+        acc += hy * hx * v1 + hy * lx * v2 + ly * hx * v3 + ly * lx * v4;
+      }
+    }
+    const float v = acc / count;
+    roi[(((size_t)r * HM + ph) * HM + pw) * TOPK + lane] = v;
+    s_sum += v;
+    s_max = fmaxf(s_max, v);
+  }
+  red[wave][0][lane] = s_sum;
+  red[wave][1][lane] = s_max;
+  __syncthreads();
+  if (wave == 0) {
+    const float s = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
+    const float m = fmaxf(fmaxf(red[0][1][lane], red[1][1][lane]), fmaxf(red[2][1][lane], red[3][1][lane]));
+    float* st = roi_stats + ((size_t)r * HM + ph) * 2 * TOPK;
+    st[lane] = s;
+    st[TOPK + lane] = m;
+  }
+}
+
+// ---------------------------------------------------------------- HeatmapHead channel attention
+// grid R, 64 threads.  cw[r][c] = sigmoid(fc(avg) + fc(max)), fc = 64->4 ReLU ->64.
+__global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__ roi_stats,
+                                                       const float* __restrict__ w0, const float* __restrict__ b0,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       float* __restrict__ cw) {
+  __shared__ float avg[TOPK], mx[TOPK], h[8];
+  const int r = blockIdx.x, c = threadIdx.x;
+  const float* st = roi_stats + (size_t)r * HM * 2 * TOPK;
+  float s = 0.f, m = -INFINITY;
+  for (int row = 0; row < HM; ++row) {
+    s += st[row * 2 * TOPK + c];
+    m = fmaxf(m, st[row * 2 * TOPK + TOPK + c]);
+  }
+  avg[c] = s / (float)HMP;
+  mx[c] = m;
+  __syncthreads();
+  if (c < 8) {
+    const int j = c & 3;
+    const float* v = (c < 4) ? avg : mx;
+    float a = b0[j];
+    for (int k = 0; k < TOPK; ++k) a = fmaf(w0[j * TOPK + k], v[k], a);
+    h[c] = fmaxf(a, 0.f);
+  }
+  __syncthreads();
+  float oa = b2[c], om = b2[c];
+  for (int j = 0; j < 4; ++j) {
+    oa = fmaf(w2[c * 4 + j], h[j], oa);
+    om = fmaf(w2[c * 4 + j], h[4 + j], om);
+  }
+  cw[(size_t)r * TOPK + c] = kpd_sigmoid(oa + om);
+}
+
+// ---------------------------------------------------------------- spatial pool
+// grid (56 rows, R), 64 threads (one output pixel x each; 56 active).
+// smap[r][y][x] = {mean_c, max_c} of roi*cw.
+__global__ __launch_bounds__(64) void hm_spool_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
+                                                      float* __restrict__ smap) {
+  __shared__ float scw[TOPK];
+  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
+  scw[x] = cw[(size_t)r * TOPK + x];
+  __syncthreads();
+  if (x >= HM) return;
+  const size_t pix = ((size_t)r * HM + y) * HM + x;
+  const float4* src = reinterpret_cast<const float4*>(roi + pix * TOPK);
+  float s = 0.f, m = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < TOPK / 4; ++q) {
+    const float4 v = src[q];
+    const float a = v.x * scw[4 * q], b = v.y * scw[4 * q + 1], c = v.z * scw[4 * q + 2], d = v.w * scw[4 * q + 3];
+    s += a; s += b; s += c; s += d;
+    m = fmaxf(fmaxf(m, a), fmaxf(b, fmaxf(c, d)));
+  }
+  smap[pix * 2 + 0] = s / (float)TOPK;
+  smap[pix * 2 + 1] = m;
+}
+
+// ---------------------------------------------------------------- spatial apply
+// grid (56 rows, R), 64 threads.  sw = sigmoid(conv7x7([mean,max]) + b);
+// xs = (roi * cw) * sw stored as the first heatmap conv's operand (bf16 or f32).
+__global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
+                                                       const float* __restrict__ smap, const float* __restrict__ saw,
+                                                       const float* __restrict__ sab, void* __restrict__ xs,
+                                                       int out_bf16) {
+  __shared__ float scw[TOPK];
+  __shared__ float w[98];
+  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
+  scw[x] = cw[(size_t)r * TOPK + x];
+  for (int i = x; i < 98; i += 64) w[i] = saw[i];
+  __syncthreads();
+  if (x >= HM) return;
+  float a = 0.f;
+  const float* sm = smap + (size_t)r * HMP * 2;
+  for (int ky = 0; ky < 7; ++ky) {
+    const int iy = y + ky - 3;
+    if (iy < 0 || iy >= HM) continue;
+    for (int kx = 0; kx < 7; ++kx) {
+      const int ix = x + kx - 3;
+      if (ix < 0 || ix >= HM) continue;
+      const float2 v = *reinterpret_cast<const float2*>(sm + (iy * HM + ix) * 2);
+      a = fmaf(w[ky * 7 + kx], v.x, a);
+      a = fmaf(w[49 + ky * 7 + kx], v.y, a);
+    }
+  }
+  const float sw = kpd_sigmoid(a + sab[0]);
+  const size_t pix = ((size_t)r * HM + y) * HM + x;
+  const float4* src = reinterpret_cast<const float4*>(roi + pix * TOPK);
+  if (out_bf16) {
+    __bf16* dst = reinterpret_cast<__bf16*>(xs) + pix * TOPK;
+#pragma unroll
+    for (int q = 0; q < TOPK / 8; ++q) {
+      const float4 u = src[2 * q], v = src[2 * q + 1];
+      bf16x8 o;
+      o[0] = (__bf16)((u.x * scw[8 * q + 0]) * sw); o[1] = (__bf16)((u.y * scw[8 * q + 1]) * sw);
+      o[2] = (__bf16)((u.z * scw[8 * q + 2]) * sw); o[3] = (__bf16)((u.w * scw[8 * q + 3]) * sw);
+      o[4] = (__bf16)((v.x * scw[8 * q + 4]) * sw); o[5] = (__bf16)((v.y * scw[8 * q + 5]) * sw);
+      o[6] = (__bf16)((v.z * scw[8 * q + 6]) * sw); o[7] = (__bf16)((v.w * scw[8 * q + 7]) * sw);
+      *reinterpret_cast<bf16x8*>(dst + 8 * q) = o;
+    }
+  } else {
+    float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(xs) + pix * TOPK);
+#pragma unroll
+    for (int q = 0; q < TOPK / 4; ++q) {
+      const float4 u = src[q];
+      dst[q] = make_float4((u.x * scw[4 * q]) * sw, (u.y * scw[4 * q + 1]) * sw, (u.z * scw[4 * q + 2]) * sw,
+                           (u.w * scw[4 * q + 3]) * sw);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- final 1x1 + sigmoid
+// grid (56 rows, R), 64 threads (pixel x).  h3: [R][3136][64] f32.
+// heat_out: [B][P][17][56][56] written at the box's compacted slot.
+__global__ __launch_bounds__(64) void hm_final_kernel(const float* __restrict__ h3, const float* __restrict__ w,
+                                                      const float* __restrict__ b, const int32_t* __restrict__ slot,
+                                                      int P, float* __restrict__ heat_out) {
+  __shared__ float sw[NK * TOPK];
+  __shared__ float sb[NK];
+  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
+  const int sl = slot[r];
+  if (sl < 0) return;  // all-zero box: skipped by the reference
+  for (int i = x; i < NK * TOPK; i += 64) sw[i] = w[i];
+  if (x < NK) sb[x] = b[x];
+  __syncthreads();
+  if (x >= HM) return;
+  const int bimg = r / P;
+  const size_t pix = ((size_t)r * HM + y) * HM + x;
+  float v[TOPK];
+  const float4* src = reinterpret_cast<const float4*>(h3 + pix * TOPK);
+#pragma unroll
+  for (int q = 0; q < TOPK / 4; ++q) {
+    const float4 u = src[q];
+    v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+  }
+  float* dst = heat_out + ((size_t)(bimg * P + sl) * NK) * HMP + y * HM + x;
+  for (int k = 0; k < NK; ++k) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < TOPK; ++c) a = fmaf(sw[k * TOPK + c], v[c], a);
+    dst[(size_t)k * HMP] = kpd_sigmoid(a + sb[k]);
+  }
+}
+
+// ---------------------------------------------------------------- decode
+// grid R, 256 threads (4 waves, each takes keypoints k = wave, wave+4, ...).
+__global__ __launch_bounds__(256) void decode_kernel(const float* __restrict__ heat_out,
+                                                     const float* __restrict__ boxes,
+                                                     const int32_t* __restrict__ slot, int P,
+                                                     float* __restrict__ kpts_out, float* __restrict__ vis_out) {
+  const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sl = slot[r];
+  if (sl < 0) return;
+  const int bimg = r / P;
+  const size_t o = (size_t)(bimg * P + sl) * NK;
+  const float cx = boxes[r * 4 + 0], cy = boxes[r * 4 + 1], bw = boxes[r * 4 + 2], bh = boxes[r * 4 + 3];
+  for (int k = wave; k < NK; k += 4) {
+    const float* hp = heat_out + (o + k) * HMP;
+    float m = -INFINITY;
+    for (int i = lane; i < HMP; i += 64) m = fmaxf(m, hp[i]);
+    m = wave_max(m);
+    float se = 0.f, sx = 0.f, sy = 0.f;
+    for (int i = lane; i < HMP; i += 64) {
+      const float e = expf(hp[i] - m);
+      se += e;
+      sx = fmaf(e, (float)(i % HM), sx);
+      sy = fmaf(e, (float)(i / HM), sy);
+    }
+    se = wave_sum(se); sx = wave_sum(sx); sy = wave_sum(sy);
+    if (lane == 0) {
+      const float kx = (sx / se) / (float)(HM - 1);
+      const float ky = (sy / se) / (float)(HM - 1);
+      const float px = fminf(fmaxf(kx * bw + (cx - bw / 2.f), 0.f), 1.f);
+      const float py = fminf(fmaxf(ky * bh + (cy - bh / 2.f), 0.f), 1.f);
+      kpts_out[(o + k) * 2 + 0] = px;
+      kpts_out[(o + k) * 2 + 1] = py;
+      const float conf = kpd_sigmoid(m);
+      const int cls = conf < 0.3f ? 0 : (conf < 0.7f ? 1 : 2);
+      vis_out[(o + k) * 3 + 0] = cls == 0 ? 1.f : 0.f;
+      vis_out[(o + k) * 3 + 1] = cls == 1 ? 1.f : 0.f;
+      vis_out[(o + k) * 3 + 2] = cls == 2 ? 1.f : 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
+                       const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st) {
+  hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(FC), 0, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores);
+  return hipGetLastError();
+}
+hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, float* vis_out, hipStream_t st) {
+  hipLaunchKernelGGL(slotmap_kernel, dim3((B + 63) / 64), dim3(64), 0, st, boxes, B, P, slot, vis_out);
+  return hipGetLastError();
+}
+hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk, const float* boxes,
+                            int R, int P, float* roi, float* roi_stats, hipStream_t st) {
+  hipLaunchKernelGGL(roi_align_kernel, dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, topk, boxes, P, roi,
+                     roi_stats);
+  return hipGetLastError();
+}
+hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,
+                            const float* b2, float* cw, hipStream_t st) {
+  hipLaunchKernelGGL(hm_chattn_kernel, dim3(R), dim3(64), 0, st, roi_stats, w0, b0, w2, b2, cw);
+  return hipGetLastError();
+}
+hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st) {
+  hipLaunchKernelGGL(hm_spool_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap);
+  return hipGetLastError();
+}
+hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
+                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st) {
+  hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16);
+  return hipGetLastError();
+}
+hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot, int P,
+                           float* heat_out, hipStream_t st) {
+  hipLaunchKernelGGL(hm_final_kernel, dim3(HM, R), dim3(64), 0, st, h3, w, b, slot, P, heat_out);
+  return hipGetLastError();
+}
+hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_t* slot, int R, int P,
+                         float* kpts_out, float* vis_out, hipStream_t st) {
+  hipLaunchKernelGGL(decode_kernel, dim3(R), dim3(256), 0, st, heat_out, boxes, slot, P, kpts_out, vis_out);
+  return hipGetLastError();
+}

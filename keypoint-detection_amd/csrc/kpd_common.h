@@ -1,0 +1,38 @@
+// Shared device/host helpers for the keypoint-detection HIP path (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+enum KpdAct : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2, ACT_HSWISH = 3, ACT_SIGMOID = 4 };
+
+// Activation formulas follow ATen's CPU kernels operation-for-operation
+// (hardswish: x * min(max(x + 3, 0), 6) / 6) so rounding matches closely.
+__device__ __forceinline__ float kpd_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_RELU6: return fminf(fmaxf(v, 0.f), 6.f);
+    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float kpd_sigmoid(float v) { return 1.f / (1.f + expf(-v)); }
+__device__ __forceinline__ float kpd_hsigmoid(float v) { return fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define KPD_CHECK_LAUNCH() (hipGetLastError())

@@ -1,0 +1,59 @@
+// Internal launcher declarations (host side of each .hip translation unit).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct ConvArgs {
+  const void* in;        // NHWC [N][H][W][in_cstride] (TA)
+  const void* wt;        // [cout_p][KS*KS][cin_p] (TA), BN folded
+  const float* bias;     // [cout_p]
+  void* out;             // NHWC [N][H][W][out_cstride] (TO)
+  const float* res;      // optional residual NHWC [N][rh][rw][cout_p] (f32), added after act
+  const float* a_scale;  // optional [N][cin_p] per-image input-channel scale (SE), f32 path only
+  float* stats;          // optional [N][tiles_per_img][2][cout_p] channel sum / max partials
+  int N, H, W;
+  int cin_p, cout_p;
+  int in_cstride, out_cstride;
+  int rh, rw;
+  int act;
+  int M;                 // N*H*W
+  int tiles_per_img;
+};
+
+enum ConvDType : int { CONV_F32 = 0, CONV_BF16_OUT_BF16 = 1, CONV_BF16_OUT_F32 = 2 };
+
+int conv_tile_m();
+hipError_t launch_conv(const ConvArgs& a, ConvDType dt, int ks, hipStream_t st);
+
+// ---- MobileNetV3 body (body_kernels.hip) ----
+hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const float* w, const float* b,
+                       float* out, int Ho, int Wo, hipStream_t st);
+hipError_t launch_dwconv(const float* in, const float* w, const float* b, float* out, int N, int H, int W,
+                         int Cp, int Ho, int Wo, int k, int s, int act, hipStream_t st);
+hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
+                     const float* w2, const float* b2, int sq, float* scale, hipStream_t st);
+hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
+                                hipStream_t st);
+
+// ---- channel attention / ROI / heatmap head / decode (head_kernels.hip) ----
+hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
+                       const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st);
+hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, float* vis_out,
+                          hipStream_t st);
+hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
+                            const float* boxes, int R, int P, float* roi, float* roi_stats,
+                            hipStream_t st);
+hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0,
+                            const float* w2, const float* b2, float* cw, hipStream_t st);
+hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st);
+hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
+                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st);
+hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot,
+                           int P, float* heat_out, hipStream_t st);
+hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_t* slot, int R, int P,
+                         float* kpts_out, float* vis_out, hipStream_t st);
+
+// ---- person head / NMS (nms.hip) ----
+hipError_t launch_nms(const float* boxes, const float* scores, int n, float thr, int max_out,
+                      int32_t* keep, int32_t* n_keep, void* scratch, size_t scratch_bytes, hipStream_t st);
+size_t nms_scratch_bytes(int n);

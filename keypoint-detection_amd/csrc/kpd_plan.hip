@@ -1,0 +1,695 @@
+// Native runtime of the keypoint-detection hot path: weight registry keyed by
+// the reference's state-dict names, BN folding + NHWC/MFMA repacking, a
+// shape-keyed device workspace, and the kernel schedule of the eval forward.
+// Exposes the C ABI declared in include/kpd.h.
+//
+// Reference call stack reproduced by kpd_forward:
+//   backbone (torchvision mobilenet_v3_small features.0..12 + LightweightFPN)
+//     dll/models/backbone.py:29-39, 258-264
+//   select_top_k_channels          dll/models/keypoint_model.py:90, 653-661
+//   per-box ROI / heatmap / decode dll/models/keypoint_model.py:143-199
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/kpd.h"
+#include "kpd_common.h"
+#include "kpd_kernels.h"
+
+hipError_t launch_nms_sets(const float* boxes, const float* scores, int sets, int n, float thr, int max_out,
+                           int max_keep, int32_t* keep, int32_t* n_keep, void* scratch, hipStream_t st);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return fail(KPD_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));               \
+  } while (0)
+
+inline int pad16(int c) { return (c + 15) / 16 * 16; }
+
+struct HostT {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+// (in, kernel, expanded, out, use_se, act(1 relu / 3 hswish), stride) -- torchvision table
+struct BneckCfg { int cin, k, exp, cout; bool se; int act, s; };
+const BneckCfg kBneck[11] = {
+    {16, 3, 16, 16, true, ACT_RELU, 2},    {16, 3, 72, 24, false, ACT_RELU, 2},
+    {24, 3, 88, 24, false, ACT_RELU, 1},   {24, 5, 96, 40, true, ACT_HSWISH, 2},
+    {40, 5, 240, 40, true, ACT_HSWISH, 1}, {40, 5, 240, 40, true, ACT_HSWISH, 1},
+    {40, 5, 120, 48, true, ACT_HSWISH, 1}, {48, 5, 144, 48, true, ACT_HSWISH, 1},
+    {48, 5, 288, 96, true, ACT_HSWISH, 2}, {96, 5, 576, 96, true, ACT_HSWISH, 1},
+    {96, 5, 576, 96, true, ACT_HSWISH, 1}};
+const int kFpnIn[4] = {16, 24, 48, 576};
+
+int se_squeeze(int c) {
+  const int v = c / 4;
+  int n = std::max(8, (int)(v + 4) / 8 * 8);
+  if (n < 0.9 * v) n += 8;
+  return n;
+}
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct DevConv {
+  int cin = 0, cout = 0, cin_p = 0, cout_p = 0, k = 1;
+  bool bf16 = false;
+  void* w = nullptr;
+  float* b = nullptr;
+};
+struct DevDW { int C = 0, Cp = 0, k = 3, s = 1, act = 0; float* w = nullptr; float* b = nullptr; };
+struct DevSE { int C = 0, Cp = 0, sq = 0; float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr; };
+struct DevBneck {
+  BneckCfg cfg;
+  bool has_exp = false;
+  DevConv expand, project;
+  DevDW dw;
+  DevSE se;
+};
+
+struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
+  float* stem = nullptr;
+  float* e[11] = {};
+  float* d[11] = {};
+  float* sesc[11] = {};
+  float* o[11] = {};
+  float* last = nullptr;
+  float* lat[4] = {};
+  float* feat = nullptr;
+  float* stats = nullptr;
+  int32_t* topk = nullptr;
+  float* scores = nullptr;
+  int32_t* slot = nullptr;
+  float* roi = nullptr;
+  float* roi_stats = nullptr;
+  float* cw = nullptr;
+  float* smap = nullptr;
+  void* xs = nullptr;
+  void* h1 = nullptr;
+  void* h2 = nullptr;
+  float* h3 = nullptr;
+  float* heat = nullptr;  // internal heat buffer when the caller passes NULL
+};
+
+struct Dims {
+  int B = 0, H = 0, W = 0, NB = 0, P = 0;
+  int h[12] = {}, w[12] = {};  // spatial dims after stem (0) and after bneck i (i+1)
+  int Hf = 0, Wf = 0, tiles = 0;
+  bool fused_stats = false;
+  bool operator==(const Dims& o) const {
+    return B == o.B && H == o.H && W == o.W && NB == o.NB && P == o.P;
+  }
+};
+
+}  // namespace
+
+struct kpd_plan {
+  int device = 0;
+  int in_ch = 3;
+  int precision = KPD_PRECISION_FP32;
+  bool finalized = false;
+  std::map<std::string, HostT> t;
+  std::vector<void*> allocs;
+  // packed device weights
+  float *stem_w = nullptr, *stem_b = nullptr;
+  DevBneck bn[11];
+  DevConv last;
+  DevConv lat[4];
+  DevConv fpn0;
+  float *ca_w0 = nullptr, *ca_b0 = nullptr, *ca_w2 = nullptr, *ca_b2 = nullptr;
+  float *hca_w0 = nullptr, *hca_b0 = nullptr, *hca_w2 = nullptr, *hca_b2 = nullptr;
+  float *sa_w = nullptr, *sa_b = nullptr;
+  DevConv hm1, hm2, hm3;
+  float *fin_w = nullptr, *fin_b = nullptr;
+  float* zero_bias = nullptr;  // 128 zeros for bias-free laterals
+  // workspace
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  Dims dims;
+  Work work;
+  bool have_work = false;
+  std::map<std::string, std::pair<const void*, size_t>> debug;
+  // per-stage HIP-event timing (kpd_plan_timing)
+  struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; size_t used = 0; };
+  bool timing = false;
+  std::map<std::string, Timer> timers;
+};
+
+namespace {
+
+// ------------------------------------------------------------------ weight helpers
+const HostT* get(kpd_plan* p, const std::string& name, std::string& missing) {
+  auto it = p->t.find(name);
+  if (it == p->t.end()) {
+    missing += name + " ";
+    return nullptr;
+  }
+  return &it->second;
+}
+
+template <typename T>
+int upload(kpd_plan* p, const std::vector<T>& h, T** out) {
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, std::max<size_t>(h.size(), 1) * sizeof(T)));
+  p->allocs.push_back(d);
+  if (!h.empty()) HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = reinterpret_cast<T*>(d);
+  return KPD_OK;
+}
+
+// BN fold: scale = gamma / sqrt(var + eps), shift = beta - mean * scale (+ conv bias * scale)
+void bn_fold(const HostT* g, const HostT* b, const HostT* m, const HostT* v, double eps, int n,
+             const HostT* conv_bias, std::vector<double>& scale, std::vector<double>& shift) {
+  scale.assign(n, 1.0);
+  shift.assign(n, 0.0);
+  for (int i = 0; i < n; ++i) {
+    const double cb = conv_bias ? conv_bias->data[i] : 0.0;
+    if (g) {
+      const double s = (double)g->data[i] / std::sqrt((double)v->data[i] + eps);
+      scale[i] = s;
+      shift[i] = (double)b->data[i] - (double)m->data[i] * s + cb * s;
+    } else {
+      shift[i] = cb;
+    }
+  }
+}
+
+// Dense conv weights [cout][cin][k][k] -> packed [cout_p][k*k][cin_p] with BN scale.
+int pack_conv(kpd_plan* p, const std::string& wname, const std::string& bias_name, const std::string& bn,
+              double eps, int k, bool bf16, DevConv& dc, std::string& missing) {
+  const HostT* w = get(p, wname, missing);
+  const HostT* cb = bias_name.empty() ? nullptr : get(p, bias_name, missing);
+  const HostT *g = nullptr, *b = nullptr, *m = nullptr, *v = nullptr;
+  if (!bn.empty()) {
+    g = get(p, bn + ".weight", missing); b = get(p, bn + ".bias", missing);
+    m = get(p, bn + ".running_mean", missing); v = get(p, bn + ".running_var", missing);
+  }
+  if (!w || (!bias_name.empty() && !cb) || (!bn.empty() && (!g || !b || !m || !v))) return KPD_ESTATE;
+  if (w->shape.size() != 4 || w->shape[2] != k || w->shape[3] != k)
+    return fail(KPD_EINVAL, "bad shape for " + wname);
+  dc.cout = (int)w->shape[0];
+  dc.cin = (int)w->shape[1];
+  dc.k = k;
+  dc.bf16 = bf16;
+  dc.cin_p = bf16 ? (dc.cin + 63) / 64 * 64 : pad16(dc.cin);
+  dc.cout_p = pad16(dc.cout);
+  std::vector<double> scale, shift;
+  bn_fold(g, b, m, v, eps, dc.cout, cb, scale, shift);
+  const int kk = k * k;
+  std::vector<float> pw((size_t)dc.cout_p * kk * dc.cin_p, 0.f);
+  for (int co = 0; co < dc.cout; ++co)
+    for (int ci = 0; ci < dc.cin; ++ci)
+      for (int t = 0; t < kk; ++t)
+        pw[((size_t)co * kk + t) * dc.cin_p + ci] =
+            (float)((double)w->data[((size_t)co * dc.cin + ci) * kk + t] * scale[co]);
+  std::vector<float> pb(dc.cout_p, 0.f);
+  for (int co = 0; co < dc.cout; ++co) pb[co] = (float)shift[co];
+  if (bf16) {
+    std::vector<uint16_t> hb(pw.size());
+    for (size_t i = 0; i < pw.size(); ++i) hb[i] = f2bf(pw[i]);
+    uint16_t* d = nullptr;
+    if (int rc = upload(p, hb, &d)) return rc;
+    dc.w = d;
+  } else {
+    float* d = nullptr;
+    if (int rc = upload(p, pw, &d)) return rc;
+    dc.w = d;
+  }
+  return upload(p, pb, &dc.b);
+}
+
+int pack_dw(kpd_plan* p, const std::string& pre, int k, int s, int act, DevDW& dw, std::string& missing) {
+  const HostT* w = get(p, pre + ".0.weight", missing);
+  const HostT *g = get(p, pre + ".1.weight", missing), *b = get(p, pre + ".1.bias", missing);
+  const HostT *m = get(p, pre + ".1.running_mean", missing), *v = get(p, pre + ".1.running_var", missing);
+  if (!w || !g || !b || !m || !v) return KPD_ESTATE;
+  dw.C = (int)w->shape[0];
+  dw.Cp = pad16(dw.C);
+  dw.k = k; dw.s = s; dw.act = act;
+  std::vector<double> scale, shift;
+  bn_fold(g, b, m, v, 1e-3, dw.C, nullptr, scale, shift);
+  std::vector<float> pw((size_t)k * k * dw.Cp, 0.f), pb(dw.Cp, 0.f);
+  for (int c = 0; c < dw.C; ++c) {
+    for (int t = 0; t < k * k; ++t) pw[(size_t)t * dw.Cp + c] = (float)(w->data[(size_t)c * k * k + t] * scale[c]);
+    pb[c] = (float)shift[c];
+  }
+  if (int rc = upload(p, pw, &dw.w)) return rc;
+  return upload(p, pb, &dw.b);
+}
+
+int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& missing, size_t expect = 0) {
+  const HostT* w = get(p, name, missing);
+  if (!w) return KPD_ESTATE;
+  if (expect && w->data.size() != expect) return fail(KPD_EINVAL, "bad size for " + name);
+  return upload(p, w->data, out);
+}
+
+// ------------------------------------------------------------------ workspace
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t n) {
+    off = (off + 255) / 256 * 256;
+    T* r = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return r;
+  }
+};
+
+size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
+  Carver c{base};
+  const int B = d.B;
+  const size_t R = (size_t)d.NB * d.P;
+  w.stem = c.take<float>((size_t)B * d.h[0] * d.w[0] * 16);
+  for (int i = 0; i < 11; ++i) {
+    const DevBneck& bn = p->bn[i];
+    const int ep = pad16(bn.cfg.exp), op = pad16(bn.cfg.cout);
+    if (bn.has_exp) w.e[i] = c.take<float>((size_t)B * d.h[i] * d.w[i] * ep);
+    w.d[i] = c.take<float>((size_t)B * d.h[i + 1] * d.w[i + 1] * ep);
+    if (bn.cfg.se) w.sesc[i] = c.take<float>((size_t)B * ep);
+    w.o[i] = c.take<float>((size_t)B * d.h[i + 1] * d.w[i + 1] * op);
+  }
+  w.last = c.take<float>((size_t)B * d.h[11] * d.w[11] * 576);
+  const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
+  for (int i = 0; i < 4; ++i) w.lat[i] = c.take<float>((size_t)B * lh[i] * lw[i] * 128);
+  w.feat = c.take<float>((size_t)B * d.Hf * d.Wf * 128);
+  w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
+  w.topk = c.take<int32_t>((size_t)B * 64);
+  w.scores = c.take<float>((size_t)B * 128);
+  if (R > 0) {
+    const size_t px = R * 3136;
+    const size_t es = p->precision == KPD_PRECISION_MIXED ? 2 : 4;
+    w.slot = c.take<int32_t>(R);
+    w.roi = c.take<float>(px * 64);
+    w.roi_stats = c.take<float>(R * 56 * 2 * 64);
+    w.cw = c.take<float>(R * 64);
+    w.smap = c.take<float>(px * 2);
+    w.xs = c.take<char>(px * 64 * es);
+    w.h1 = c.take<char>(px * 256 * es);
+    w.h2 = c.take<char>(px * 256 * es);
+    w.h3 = c.take<float>(px * 64);
+    w.heat = c.take<float>(R * 17 * 3136);
+  }
+  return c.off + 256;
+}
+
+// RAII stage marker: records a start/end event pair on the launch stream
+// when timing is enabled (events are pooled per stage and reused).
+struct Stage {
+  kpd_plan* p;
+  hipStream_t st;
+  hipEvent_t end = nullptr;
+  Stage(kpd_plan* plan, const char* name, hipStream_t stream) : p(plan), st(stream) {
+    if (!p->timing) return;
+    auto& t = p->timers[name];
+    if (t.used == t.ev.size()) {
+      hipEvent_t a, b;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      t.ev.emplace_back(a, b);
+    }
+    auto& pr = t.ev[t.used++];
+    (void)hipEventRecord(pr.first, st);
+    end = pr.second;
+  }
+  ~Stage() {
+    if (end) (void)hipEventRecord(end, st);
+  }
+};
+
+int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, void* out, int act,
+         const float* res, int rh, int rw, const float* a_scale, float* stats, int tiles, int out_kind,
+         hipStream_t st) {
+  ConvArgs a{};
+  a.in = in; a.wt = L.w; a.bias = L.b; a.out = out; a.res = res; a.a_scale = a_scale; a.stats = stats;
+  a.N = N; a.H = H; a.W = W; a.cin_p = L.cin_p; a.cout_p = L.cout_p;
+  a.in_cstride = in_cstride; a.out_cstride = L.cout_p;
+  a.rh = rh; a.rw = rw; a.act = act; a.M = N * H * W; a.tiles_per_img = tiles;
+  const ConvDType dt = !L.bf16 ? CONV_F32 : (out_kind == 1 ? CONV_BF16_OUT_BF16 : CONV_BF16_OUT_F32);
+  HIP_TRY(launch_conv(a, dt, L.k, st));
+  return KPD_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* kpd_last_error(void) { return g_err.c_str(); }
+const char* kpd_version(void) { return "kpd 0.1 gfx950"; }
+
+int kpd_plan_create(int device, int in_channels, kpd_plan** out) {
+  if (!out) return fail(KPD_EINVAL, "out is NULL");
+  if (in_channels != 1 && in_channels != 3) return fail(KPD_EINVAL, "in_channels must be 1 or 3");
+  auto* p = new kpd_plan();
+  p->device = device;
+  p->in_ch = in_channels;
+  *out = p;
+  return KPD_OK;
+}
+
+int kpd_plan_set_tensor(kpd_plan* p, const char* name, const float* host, const int64_t* shape, int ndim) {
+  if (!p || !name || (!host && ndim > 0)) return fail(KPD_EINVAL, "null argument");
+  HostT t;
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    if (shape[i] < 0) return fail(KPD_EINVAL, "negative dim");
+    t.shape.push_back(shape[i]);
+    n *= (size_t)shape[i];
+  }
+  t.data.assign(host, host + n);
+  p->t[name] = std::move(t);
+  p->finalized = false;
+  return KPD_OK;
+}
+
+void kpd_plan_destroy(kpd_plan* p) {
+  if (!p) return;
+  int cur = 0;
+  if (hipGetDevice(&cur) == hipSuccess) (void)hipSetDevice(p->device);
+  for (void* a : p->allocs) (void)hipFree(a);
+  if (p->ws) (void)hipFree(p->ws);
+  for (auto& kv : p->timers)
+    for (auto& e : kv.second.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  (void)hipSetDevice(cur);
+  delete p;
+}
+
+int kpd_plan_finalize(kpd_plan* p, int precision) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  if (precision != KPD_PRECISION_FP32 && precision != KPD_PRECISION_MIXED)
+    return fail(KPD_EINVAL, "unknown precision");
+  HIP_TRY(hipSetDevice(p->device));
+  for (void* a : p->allocs) (void)hipFree(a);
+  p->allocs.clear();
+  if (p->ws) { (void)hipFree(p->ws); p->ws = nullptr; p->ws_bytes = 0; }
+  p->have_work = false;
+  p->precision = precision;
+  std::string missing;
+  int rc = KPD_OK;
+  auto chk = [&](int r) { if (r != KPD_OK && rc == KPD_OK) rc = r; };
+  const std::string F = "backbone.body.features.";
+  // stem: [16][Cin][3][3] + BN, packed [16][Cin*9]
+  {
+    const HostT* w = get(p, F + "0.0.weight", missing);
+    const HostT *g = get(p, F + "0.1.weight", missing), *b = get(p, F + "0.1.bias", missing);
+    const HostT *m = get(p, F + "0.1.running_mean", missing), *v = get(p, F + "0.1.running_var", missing);
+    if (w && g && b && m && v) {
+      if (w->shape.size() != 4 || w->shape[0] != 16 || w->shape[1] != p->in_ch)
+        return fail(KPD_EINVAL, "stem weight shape does not match in_channels");
+      std::vector<double> sc, sh;
+      bn_fold(g, b, m, v, 1e-3, 16, nullptr, sc, sh);
+      std::vector<float> pw(w->data.size()), pb(16);
+      const size_t per = w->data.size() / 16;
+      for (int co = 0; co < 16; ++co) {
+        for (size_t k = 0; k < per; ++k) pw[co * per + k] = (float)(w->data[co * per + k] * sc[co]);
+        pb[co] = (float)sh[co];
+      }
+      chk(upload(p, pw, &p->stem_w));
+      chk(upload(p, pb, &p->stem_b));
+    } else {
+      chk(KPD_ESTATE);
+    }
+  }
+  for (int i = 0; i < 11; ++i) {
+    DevBneck& bn = p->bn[i];
+    bn.cfg = kBneck[i];
+    bn.has_exp = bn.cfg.exp != bn.cfg.cin;
+    const std::string pre = F + std::to_string(i + 1) + ".block.";
+    int j = 0;
+    if (bn.has_exp) {
+      chk(pack_conv(p, pre + "0.0.weight", "", pre + "0.1", 1e-3, 1, false, bn.expand, missing));
+      ++j;
+    }
+    chk(pack_dw(p, pre + std::to_string(j), bn.cfg.k, bn.cfg.s, bn.cfg.act, bn.dw, missing));
+    ++j;
+    if (bn.cfg.se) {
+      const std::string s = pre + std::to_string(j);
+      bn.se.C = bn.cfg.exp; bn.se.Cp = pad16(bn.cfg.exp); bn.se.sq = se_squeeze(bn.cfg.exp);
+      chk(pack_plain(p, s + ".fc1.weight", &bn.se.w1, missing, (size_t)bn.se.sq * bn.se.C));
+      chk(pack_plain(p, s + ".fc1.bias", &bn.se.b1, missing, bn.se.sq));
+      chk(pack_plain(p, s + ".fc2.weight", &bn.se.w2, missing, (size_t)bn.se.sq * bn.se.C));
+      chk(pack_plain(p, s + ".fc2.bias", &bn.se.b2, missing, bn.se.C));
+      ++j;
+    }
+    const std::string pj = pre + std::to_string(j);
+    chk(pack_conv(p, pj + ".0.weight", "", pj + ".1", 1e-3, 1, false, bn.project, missing));
+  }
+  chk(pack_conv(p, F + "12.0.weight", "", F + "12.1", 1e-3, 1, false, p->last, missing));
+  for (int i = 0; i < 4; ++i)
+    chk(pack_conv(p, "backbone.fpn.lateral_convs." + std::to_string(i) + ".weight", "", "", 0, 1, false,
+                  p->lat[i], missing));
+  chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
+                p->fpn0, missing));
+  chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
+  chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
+  chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
+  chk(pack_plain(p, "channel_attention.fc.2.bias", &p->ca_b2, missing, 128));
+  const std::string Hh = "heatmap_head.";
+  chk(pack_plain(p, Hh + "channel_attention.fc.0.weight", &p->hca_w0, missing, 4 * 64));
+  chk(pack_plain(p, Hh + "channel_attention.fc.0.bias", &p->hca_b0, missing, 4));
+  chk(pack_plain(p, Hh + "channel_attention.fc.2.weight", &p->hca_w2, missing, 64 * 4));
+  chk(pack_plain(p, Hh + "channel_attention.fc.2.bias", &p->hca_b2, missing, 64));
+  chk(pack_plain(p, Hh + "spatial_attention.conv.weight", &p->sa_w, missing, 98));
+  chk(pack_plain(p, Hh + "spatial_attention.conv.bias", &p->sa_b, missing, 1));
+  const bool bf = precision == KPD_PRECISION_MIXED;
+  chk(pack_conv(p, Hh + "deconv_layers.0.weight", Hh + "deconv_layers.0.bias", Hh + "deconv_layers.1", 1e-5, 3,
+                bf, p->hm1, missing));
+  chk(pack_conv(p, Hh + "deconv_layers.4.weight", Hh + "deconv_layers.4.bias", Hh + "deconv_layers.5", 1e-5, 3,
+                bf, p->hm2, missing));
+  chk(pack_conv(p, Hh + "final_layer.0.weight", Hh + "final_layer.0.bias", Hh + "final_layer.1", 1e-5, 3, bf,
+                p->hm3, missing));
+  chk(pack_plain(p, Hh + "final_layer.3.weight", &p->fin_w, missing, 17 * 64));
+  chk(pack_plain(p, Hh + "final_layer.3.bias", &p->fin_b, missing, 17));
+  {
+    std::vector<float> z(128, 0.f);
+    chk(upload(p, z, &p->zero_bias));
+  }
+  if (!missing.empty()) return fail(KPD_ESTATE, "missing tensors: " + missing);
+  if (rc != KPD_OK) return rc;
+  // shape checks the kernels rely on
+  if (p->fpn0.cin != 128 || p->fpn0.cout != 128) return fail(KPD_EINVAL, "fpn_convs.0 must be 128->128");
+  if (p->hm1.cin != 64 || p->hm3.cout != 64 || p->hm1.cout != p->hm2.cin || p->hm2.cout != p->hm3.cin)
+    return fail(KPD_EINVAL, "heatmap head channel chain mismatch");
+  if (p->bn[0].cfg.cin != 16) return fail(KPD_EINVAL, "bad body");
+  p->finalized = true;
+  return KPD_OK;
+}
+
+static int ensure_work(kpd_plan* p, const Dims& d) {
+  if (p->have_work && p->dims == d) return KPD_OK;
+  Work w;
+  const size_t need = carve(p, d, nullptr, w);
+  if (need > p->ws_bytes) {
+    if (p->ws) HIP_TRY(hipFree(p->ws));
+    p->ws = nullptr;
+    HIP_TRY(hipMalloc(&p->ws, need));
+    p->ws_bytes = need;
+  }
+  carve(p, d, reinterpret_cast<char*>(p->ws), p->work);
+  p->dims = d;
+  p->have_work = true;
+  return KPD_OK;
+}
+
+int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, const float* boxes, int NB, int P,
+                float* kpts, float* vis, float* heat, int32_t* topk_out, void* stream) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
+  if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
+  if (NB < 0 || NB > B || P < 0) return fail(KPD_EINVAL, "bad box batch");
+  if (NB * P > 0 && (!boxes || !kpts || !vis)) return fail(KPD_EINVAL, "null box/output pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+
+  Dims d;
+  d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P;
+  d.h[0] = (H - 1) / 2 + 1; d.w[0] = (W - 1) / 2 + 1;
+  for (int i = 0; i < 11; ++i) {
+    const int k = kBneck[i].k, s = kBneck[i].s, pd = (k - 1) / 2;
+    d.h[i + 1] = (d.h[i] + 2 * pd - k) / s + 1;
+    d.w[i + 1] = (d.w[i] + 2 * pd - k) / s + 1;
+  }
+  d.Hf = d.h[0]; d.Wf = d.w[0];
+  const int HWf = d.Hf * d.Wf, TM = conv_tile_m();
+  d.fused_stats = (HWf % TM) == 0;
+  d.tiles = d.fused_stats ? HWf / TM : std::min(64, HWf);
+  if (int rc = ensure_work(p, d)) return rc;
+  Work& w = p->work;
+  p->debug.clear();
+
+  // ---------------- MobileNetV3-Small body ----------------
+  std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
+  HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], st));
+  const float* x = w.stem;
+  const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 11; ++i) {
+    const DevBneck& bn = p->bn[i];
+    const int hi = d.h[i], wi = d.w[i], ho = d.h[i + 1], wo = d.w[i + 1];
+    const int inp = pad16(bn.cfg.cin);
+    const float* e = x;
+    if (bn.has_exp) {
+      if (int rc = conv(bn.expand, x, B, hi, wi, inp, w.e[i], bn.cfg.act, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+        return rc;
+      e = w.e[i];
+    }
+    HIP_TRY(launch_dwconv(e, bn.dw.w, bn.dw.b, w.d[i], B, hi, wi, bn.dw.Cp, ho, wo, bn.dw.k, bn.dw.s, bn.dw.act, st));
+    if (bn.cfg.se)
+      HIP_TRY(launch_se(w.d[i], B, ho * wo, bn.se.C, bn.se.Cp, bn.se.w1, bn.se.b1, bn.se.w2, bn.se.b2, bn.se.sq,
+                        w.sesc[i], st));
+    const bool res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
+    if (int rc = conv(bn.project, w.d[i], B, ho, wo, bn.dw.Cp, w.o[i], ACT_NONE, res ? x : nullptr, ho, wo,
+                      bn.cfg.se ? w.sesc[i] : nullptr, nullptr, 0, 0, st))
+      return rc;
+    x = w.o[i];
+    if (i + 1 == 3) taps[1] = x;
+    if (i + 1 == 8) taps[2] = x;
+  }
+  if (int rc = conv(p->last, x, B, d.h[11], d.w[11], pad16(96), w.last, ACT_HSWISH, nullptr, 0, 0, nullptr,
+                    nullptr, 0, 0, st))
+    return rc;
+  taps[3] = w.last;
+  body_stage.reset();
+
+  // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
+  const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
+  std::unique_ptr<Stage> lat_stage(new Stage(p, "fpn_lateral", st));
+  for (int i = 3; i >= 0; --i) {
+    const DevConv& L = p->lat[i];
+    const float* res = i < 3 ? w.lat[i + 1] : nullptr;
+    if (int rc = conv(L, taps[i], B, lh[i], lw[i], pad16(kFpnIn[i]), w.lat[i], ACT_NONE, res,
+                      i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+  }
+  lat_stage.reset();
+  std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
+  if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
+                    d.fused_stats ? w.stats : nullptr, d.tiles, 0, st))
+    return rc;
+  fpn_stage.reset();
+  std::unique_ptr<Stage> topk_stage(new Stage(p, "topk", st));
+  if (!d.fused_stats) HIP_TRY(launch_channel_stats(w.feat, B, HWf, 128, d.tiles, w.stats, st));
+  HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st));
+  topk_stage.reset();
+  if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
+  p->debug["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
+  p->debug["scores"] = {w.scores, sizeof(float) * (size_t)B * 128};
+  p->debug["tap0"] = {taps[0], sizeof(float) * (size_t)B * lh[0] * lw[0] * 16};
+  p->debug["tap1"] = {taps[1], sizeof(float) * (size_t)B * lh[1] * lw[1] * pad16(24)};
+  p->debug["tap2"] = {taps[2], sizeof(float) * (size_t)B * lh[2] * lw[2] * pad16(48)};
+  p->debug["tap3"] = {taps[3], sizeof(float) * (size_t)B * lh[3] * lw[3] * 576};
+
+  const int R = NB * P;
+  if (R == 0) return KPD_OK;
+
+  // ---------------- per-ROI heads ----------------
+  float* heat_out = heat ? heat : w.heat;
+  const size_t nkp = (size_t)R * 17;
+  HIP_TRY(hipMemsetAsync(kpts, 0, nkp * 2 * sizeof(float), st));
+  HIP_TRY(hipMemsetAsync(vis, 0, nkp * 3 * sizeof(float), st));
+  HIP_TRY(hipMemsetAsync(heat_out, 0, nkp * 3136 * sizeof(float), st));
+  {
+    Stage sg(p, "roi_align", st);
+    HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, vis, st));
+    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
+  }
+  p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
+  std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
+  HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw, st));
+  HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
+  const bool bf = p->precision == KPD_PRECISION_MIXED;
+  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, bf ? 1 : 0, st));
+  att_stage.reset();
+  std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
+  if (int rc = conv(p->hm1, w.xs, R, 56, 56, 64, w.h1, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 1, st))
+    return rc;
+  c1.reset();
+  std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
+  if (int rc = conv(p->hm2, w.h1, R, 56, 56, p->hm1.cout_p, w.h2, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 1,
+                    st))
+    return rc;
+  c2.reset();
+  std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
+  if (int rc = conv(p->hm3, w.h2, R, 56, 56, p->hm2.cout_p, w.h3, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 2,
+                    st))
+    return rc;
+  c3.reset();
+  {
+    Stage sg(p, "hm_final_decode", st);
+    HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
+    HIP_TRY(launch_decode(heat_out, boxes, w.slot, R, P, kpts, vis, st));
+  }
+  return KPD_OK;
+}
+
+int kpd_plan_timing(kpd_plan* p, int enable) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  p->timing = enable != 0;
+  for (auto& kv : p->timers) kv.second.used = 0;
+  return KPD_OK;
+}
+
+int kpd_plan_timing_query(kpd_plan* p, const char* stage, double* total_ms, int* count) {
+  if (!p || !stage || !total_ms || !count) return fail(KPD_EINVAL, "null argument");
+  *total_ms = 0.0;
+  *count = 0;
+  auto it = p->timers.find(stage);
+  if (it == p->timers.end()) return KPD_OK;
+  for (size_t i = 0; i < it->second.used; ++i) {
+    auto& e = it->second.ev[i];
+    HIP_TRY(hipEventSynchronize(e.second));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
+    *total_ms += ms;
+  }
+  *count = (int)it->second.used;
+  return KPD_OK;
+}
+
+int kpd_debug_copy(kpd_plan* p, const char* name, void* dst, size_t bytes, size_t* size_out, void* stream) {
+  if (!p || !name) return fail(KPD_EINVAL, "null argument");
+  auto it = p->debug.find(name);
+  if (it == p->debug.end()) return fail(KPD_EINVAL, std::string("no debug buffer ") + name);
+  if (size_out) *size_out = it->second.second;
+  if (!dst) return KPD_OK;
+  if (bytes < it->second.second) return fail(KPD_EINVAL, "destination too small");
+  HIP_TRY(hipMemcpyAsync(dst, it->second.first, it->second.second, hipMemcpyDeviceToDevice,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return KPD_OK;
+}
+
+int kpd_nms(const float* boxes, const float* scores, int n, float thr, int max_out, int32_t* keep, int32_t* n_keep,
+            void* stream) {
+  if (n < 0 || (n > 0 && (!boxes || !scores || !keep)) || !n_keep) return fail(KPD_EINVAL, "bad nms args");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  void* scratch = nullptr;
+  if (n > 0) HIP_TRY(hipMallocAsync(&scratch, (size_t)n, st));
+  const hipError_t e = launch_nms_sets(boxes, scores, 1, n, thr, max_out, std::max(n, 1), keep, n_keep, scratch, st);
+  if (scratch) HIP_TRY(hipFreeAsync(scratch, st));
+  HIP_TRY(e);
+  return KPD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,186 @@
+"""HIP path vs the oracle / reference goldens, through the C ABI (libkpd.so).
+
+Tolerances (stated per BASELINE.md / SURVEY §8(d)):
+  precision="fp32":  max|dkpt| <= 1e-5, heatmaps atol 5e-5, top-k indices and
+                     visibility classes identical.
+  precision="mixed": max|dkpt| <= 1e-3, heatmaps atol 3e-2, top-k identical
+                     (backbone stays fp32), visibility flips reported and
+                     bounded (<= 2% of keypoints).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import kpd_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _np(p):
+    return np.load(p, allow_pickle=False)
+
+
+def _model(sd, precision="fp32", in_channels=3):
+    from dll.configs import BackboneConfig, ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    m = MultiPersonKeypointModel(ModelConfig(backbone=BackboneConfig(in_channels=in_channels)), TrainingConfig(),
+                                 precision=precision)
+    m.load_state_dict(sd)
+    return m.to(DEV).eval()
+
+
+def _nchw_feat(plan, B, Hf, Wf):
+    f = plan.debug_buffer("feat0").view(B, Hf, Wf, 128)
+    return f.permute(0, 3, 1, 2).cpu()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_forward_main_vs_golden(golden_dir, model_sd, precision):
+    from dll.models.synthetic import synthetic_images
+    g = _np(golden_dir / "forward_main.npz")
+    m = _model(model_sd, precision)
+    img = synthetic_images(2, 3, 256, 192, seed=1234, device=DEV)
+    boxes = torch.from_numpy(g["boxes"]).to(DEV)
+    with torch.no_grad():
+        out = m({"image": img, "bboxes": boxes})
+    torch.cuda.synchronize()
+    plan = m.native_plan(DEV)
+    f = _nchw_feat(plan, 2, 128, 96)
+    np.testing.assert_allclose(f.mean(dim=(2, 3)).numpy(), g["feat0_chan_mean"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(f.amax(dim=(2, 3)).numpy(), g["feat0_chan_max"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(f[:, :, 60:64, 40:44].numpy(), g["feat0_slice"], rtol=1e-4, atol=1e-4)
+    scores = plan.debug_buffer("scores").view(2, 128).cpu()
+    np.testing.assert_allclose(scores.numpy(), g["scores"], atol=1e-6)
+    topk = torch.topk(scores, 64, dim=1).indices
+    assert (topk.numpy() == g["topk"]).all()
+    kp = out["keypoints"].cpu().numpy()
+    vis = out["visibilities"].cpu().numpy()
+    hm = out["heatmap"].cpu()
+    assert kp.shape == g["keypoints"].shape and vis.shape == g["visibilities"].shape
+    if precision == "fp32":
+        np.testing.assert_allclose(kp, g["keypoints"], atol=1e-5)
+        assert (vis == g["visibilities"]).all()
+        np.testing.assert_allclose(hm[0, 0].numpy(), g["heatmap_b0p0"], atol=5e-5)
+        np.testing.assert_allclose(hm.amax(dim=(3, 4)).numpy(), g["heatmap_max"], atol=5e-5)
+    else:
+        np.testing.assert_allclose(kp, g["keypoints"], atol=1e-3)
+        flips = int((vis != g["visibilities"]).any(axis=-1).sum())
+        assert flips <= 0.02 * vis[..., 0].size
+        np.testing.assert_allclose(hm[0, 0].numpy(), g["heatmap_b0p0"], atol=3e-2)
+    # compacted + padded slot of the zero box (image 1, slot 2) is all zero
+    assert not out["keypoints"][1, 2].any() and not out["visibilities"][1, 2].any()
+
+
+def test_forward_dummy_empty(golden_dir, model_sd):
+    from dll.models.synthetic import synthetic_images
+    m = _model(model_sd)
+    img = synthetic_images(2, 3, 256, 192, seed=1234, device=DEV)
+    g = _np(golden_dir / "forward_dummy.npz")
+    with torch.no_grad():
+        out = m({"image": img, "bboxes": torch.from_numpy(g["boxes"]).to(DEV)})
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), g["keypoints"], atol=1e-5)
+    assert (out["visibilities"].cpu().numpy() == g["visibilities"]).all()
+    np.testing.assert_allclose(out["heatmap"].double().sum(dim=(3, 4)).cpu().numpy(), g["heatmap_sum"],
+                               rtol=1e-4, atol=2e-2)
+    e = _np(golden_dir / "forward_empty.npz")
+    with torch.no_grad():
+        out = m({"image": img, "bboxes": torch.zeros(2, 0, 4, device=DEV)})
+    assert tuple(out["visibilities"].shape) == tuple(e["vshape"])
+    assert tuple(out["keypoints"].shape) == tuple(e["kshape"])
+    with torch.no_grad():
+        out = m({"image": img, "bboxes": None})
+    assert tuple(out["heatmap"].shape) == tuple(e["hshape"])
+
+
+def test_forward_gray_list(golden_dir, model_sd_gray):
+    from dll.models.synthetic import synthetic_images
+    g = _np(golden_dir / "forward_gray_list.npz")
+    m = _model(model_sd_gray, in_channels=1)
+    img = synthetic_images(1, 1, 224, 224, seed=99, device=DEV)
+    with torch.no_grad():
+        out = m({"image": img, "bboxes": [torch.from_numpy(g["boxes"]).to(DEV)]})
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), g["keypoints"], atol=1e-5)
+    assert (out["visibilities"].cpu().numpy() == g["visibilities"]).all()
+    scores = m.native_plan(DEV).debug_buffer("scores").view(1, 128).cpu()
+    np.testing.assert_allclose(scores.numpy(), g["scores"], atol=1e-6)
+
+
+def test_odd_size_vs_oracle(model_sd):
+    """H/2*W/2 not a multiple of the conv M-tile -> separate channel-stats path;
+    boxes touching the border and degenerate (sub-pixel) boxes."""
+    from dll.models.synthetic import synthetic_images
+    img = synthetic_images(2, 3, 200, 152, seed=5)
+    boxes = torch.tensor([[[0.5, 0.5, 0.9, 0.95], [0.02, 0.03, 0.1, 0.1], [0.98, 0.97, 0.3, 0.4]],
+                          [[0.3, 0.6, 0.001, 0.002], [0.5, 0.5, 1.0, 1.0], [0.7, 0.2, 0.4, 0.3]]])
+    ref = O.forward(model_sd, {"image": img, "bboxes": boxes}, return_debug=True)
+    m = _model(model_sd)
+    with torch.no_grad():
+        out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
+    np.testing.assert_allclose(out["heatmap"].cpu().numpy(), ref["heatmap"].numpy(), atol=5e-5)
+
+
+def test_roi_features_vs_oracle(model_sd):
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(2, 3, 256, 192, seed=21)
+    boxes = synthetic_boxes(2, 2, seed=22)
+    m = _model(model_sd)
+    with torch.no_grad():
+        m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    plan = m.native_plan(DEV)
+    roi = plan.debug_buffer("roi").view(4, 56, 56, 64).permute(0, 3, 1, 2).cpu()
+    feat = _nchw_feat(plan, 2, 128, 96)
+    feats, _ = O.select_top_k(feat, model_sd)   # same features -> isolates roi_align + gather
+    for r in range(4):
+        b, p = divmod(r, 2)
+        want = O.extract_roi_features(feats[b:b + 1], boxes[b, p])[0]
+        np.testing.assert_allclose(roi[r].numpy(), want.numpy(), atol=2e-5)
+
+
+def test_batch_independence(model_sd):
+    """Images are independent: a batch equals its images run one at a time."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(6, 3, 256, 192, seed=31, device=DEV)
+    boxes = synthetic_boxes(6, 2, seed=32, device=DEV)
+    m = _model(model_sd)
+    with torch.no_grad():
+        full = m({"image": img, "bboxes": boxes})
+        for i in (0, 3, 5):
+            one = m({"image": img[i:i + 1], "bboxes": boxes[i:i + 1]})
+            assert torch.equal(one["keypoints"][0], full["keypoints"][i])
+            assert torch.equal(one["heatmap"][0], full["heatmap"][i])
+
+
+def test_bench_batch_properties(model_sd):
+    """BASELINE C2 shape (B=64, 256x192, 1 box): size-independent properties +
+    first images against the oracle."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(64, 3, 256, 192, seed=1234)
+    boxes = synthetic_boxes(64, 1, seed=1235)
+    m = _model(model_sd, "mixed")
+    with torch.no_grad():
+        out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    kp = out["keypoints"].cpu()
+    vis = out["visibilities"].cpu()
+    assert kp.shape == (64, 1, 1, 17, 2) and ((kp >= 0) & (kp <= 1)).all()
+    assert torch.equal(vis.sum(-1), torch.ones(64, 1, 1, 17))
+    ref = O.forward(model_sd, {"image": img[:2], "bboxes": boxes[:2]})
+    np.testing.assert_allclose(kp[:2].numpy(), ref["keypoints"].numpy(), atol=1e-3)
+
+
+def test_nms_gpu_vs_golden(golden_dir):
+    from dll.configs import PersonDetectionConfig
+    from dll.models import PERSON_HEAD
+    ph = PERSON_HEAD(PersonDetectionConfig())
+    g = _np(golden_dir / "nms.npz")
+    i = 0
+    while f"c{i}_boxes" in g:
+        mo = int(g[f"c{i}_max_out"])
+        keep = ph.non_max_suppression(torch.from_numpy(g[f"c{i}_boxes"]).to(DEV),
+                                      torch.from_numpy(g[f"c{i}_scores"]).to(DEV),
+                                      float(g[f"c{i}_thr"]), None if mo < 0 else mo)
+        assert keep.tolist() == g[f"c{i}_keep"].tolist(), f"case {i}"
+        i += 1
