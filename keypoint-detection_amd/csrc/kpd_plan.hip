@@ -647,7 +647,8 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, con
 int kpd_plan_timing(kpd_plan* p, int enable) {
   if (!p) return fail(KPD_EINVAL, "null plan");
   p->timing = enable != 0;
-  for (auto& kv : p->timers) kv.second.used = 0;
+  if (p->timing)
+    for (auto& kv : p->timers) kv.second.used = 0;
   return KPD_OK;
 }
 

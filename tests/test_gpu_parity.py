@@ -179,8 +179,14 @@ def test_nms_gpu_vs_golden(golden_dir):
     i = 0
     while f"c{i}_boxes" in g:
         mo = int(g[f"c{i}_max_out"])
-        keep = ph.non_max_suppression(torch.from_numpy(g[f"c{i}_boxes"]).to(DEV),
-                                      torch.from_numpy(g[f"c{i}_scores"]).to(DEV),
-                                      float(g[f"c{i}_thr"]), None if mo < 0 else mo)
-        assert keep.tolist() == g[f"c{i}_keep"].tolist(), f"case {i}"
+        sc = g[f"c{i}_scores"]
+        keep = ph.non_max_suppression(torch.from_numpy(g[f"c{i}_boxes"]).to(DEV), torch.from_numpy(sc).to(DEV),
+                                      float(g[f"c{i}_thr"]), None if mo < 0 else mo).tolist()
+        ref = g[f"c{i}_keep"].tolist()
+        if keep != ref:
+            # torch's CPU sort(descending) is unstable, so the reference's order
+            # among exactly tied scores is unspecified; ours is lower-index-first.
+            # Accept only a permutation among equal scores.
+            assert [sc[k] for k in keep] == [sc[k] for k in ref], f"case {i}"
+            assert sorted(keep) == sorted(ref), f"case {i}"
         i += 1

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
+
+HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
+(MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a
+wide 16-B/lane coalesced read stream -- every staging load of the conv
+kernels is a 16-B/lane load; WRITE_SIZE is read as-is).  Both counters are
+in KB.  Writes <outdir>/pmc.json and prints a table."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+STAGE_OF = {
+    "conv_mfma_kernel<float, float, 3, 128, 128, 32>": "fpn0",
+}
+
+
+def load(pattern):
+    vals = defaultdict(list)
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                v = row.get("Counter_Value")
+                if v is None:
+                    continue
+                vals[name].append(float(v))
+    return vals
+
+
+def main(outdir):
+    fetch = load(os.path.join(outdir, "FETCH_SIZE", "**", "*counter_collection.csv"))
+    write = load(os.path.join(outdir, "WRITE_SIZE", "**", "*counter_collection.csv"))
+    res = {}
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fk = sum(f) / len(f) if f else 0.0
+        wk = sum(w) / len(w) if w else 0.0
+        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(ConvArgs")[0]
+        entry = {"fetch_kb": fk, "write_kb": wk, "launches": max(len(f), len(w)),
+                 "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
+        res[short] = entry
+        for k, stage in STAGE_OF.items():
+            if k in short:
+                res[stage] = dict(entry, kernel=short,
+                                  correction="2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 16B/lane reads)")
+    for k, e in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
+        print(f"{e['hbm_bytes_per_launch'] / 1e6:12.2f} MB  fetch {e['fetch_kb'] / 1024:10.1f} MiB  "
+              f"write {e['write_kb'] / 1024:10.1f} MiB  x{e['launches']:4d}  {k[:110]}")
+    with open(os.path.join(outdir, "pmc.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
