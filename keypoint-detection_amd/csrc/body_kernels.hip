@@ -119,18 +119,32 @@ __global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, in
     mean[tid * 4 + 2] = t.z / hw; mean[tid * 4 + 3] = t.w / hw;
   }
   __syncthreads();
+  // fc1 / fc2: one thread per output streaming its weight row with 16-byte
+  // loads (C and sq are multiples of 4 in MobileNetV3-Small), two partial sums.
   for (int j = tid; j < sq; j += 256) {
-    float a = b1[j];
-    for (int c = 0; c < C; ++c) a = fmaf(w1[j * C + c], mean[c], a);
-    hid[j] = fmaxf(a, 0.f);
+    const float4* wr = reinterpret_cast<const float4*>(w1 + (size_t)j * C);
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll 4
+    for (int q = 0; q < C / 4; ++q) {
+      const float4 w = wr[q];
+      a0 = fmaf(w.x, mean[4 * q], a0); a1 = fmaf(w.y, mean[4 * q + 1], a1);
+      a0 = fmaf(w.z, mean[4 * q + 2], a0); a1 = fmaf(w.w, mean[4 * q + 3], a1);
+    }
+    hid[j] = fmaxf(a0 + a1 + b1[j], 0.f);
   }
   __syncthreads();
   for (int c = tid; c < Cp; c += 256) {
     float v = 0.f;
     if (c < C) {
-      float a = b2[c];
-      for (int j = 0; j < sq; ++j) a = fmaf(w2[c * sq + j], hid[j], a);
-      v = kpd_hsigmoid(a);
+      const float4* wr = reinterpret_cast<const float4*>(w2 + (size_t)c * sq);
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 4
+      for (int q = 0; q < sq / 4; ++q) {
+        const float4 w = wr[q];
+        a0 = fmaf(w.x, hid[4 * q], a0); a1 = fmaf(w.y, hid[4 * q + 1], a1);
+        a0 = fmaf(w.z, hid[4 * q + 2], a0); a1 = fmaf(w.w, hid[4 * q + 3], a1);
+      }
+      v = kpd_hsigmoid(a0 + a1 + b2[c]);
     }
     scale[(size_t)n * Cp + c] = v;
   }
@@ -180,7 +194,7 @@ hipError_t launch_dwconv(const float* in, const float* w, const float* b, float*
 
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st) {
-  if (Cp > 1024 || sq > 256) return hipErrorInvalidValue;
+  if (Cp > 1024 || sq > 256 || C % 4 || sq % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(se_kernel, dim3(N), dim3(256), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale);
   return hipGetLastError();
 }

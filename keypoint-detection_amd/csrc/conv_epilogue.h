@@ -1,0 +1,100 @@
+// Conv epilogue shared by the MFMA conv kernels: the block's accumulator tile
+// is staged through LDS so that every global store is a 16-byte-per-lane,
+// full-row store (a 16x16 MFMA fragment alone would give 64-byte segments),
+// and bias / activation / residual / channel statistics are applied in the
+// coalesced pass.
+#pragma once
+#include "kpd_common.h"
+
+struct EpiArgs {
+  const float* bias;   // [cout_p]
+  void* out;           // NHWC rows of out_cstride elements
+  const float* res;    // optional residual NHWC [N][rh][rw][cout_p] (nearest-upsampled when rh != H)
+  float* stats;        // optional [N][tiles_per_img][2][cout_p] (requires HW % BM == 0)
+  float* amax;         // optional atomicMax of |out|
+  float scale;         // acc multiplier before bias (split16 unscale), 1 otherwise
+  int M, H, W, cout_p, out_cstride, rh, rw, act, tiles_per_img;
+};
+
+template <int BM, int BN>
+constexpr int epi_lds_bytes() { return BM * (BN + 4) * 4; }
+
+// acc[FM][FN] of wave (wm, wn) -> LDS tile [BM][BN+4] (fp32)
+template <int FM, int FN, int WM, int WN, int BN>
+__device__ __forceinline__ void acc_to_lds(float* tile, const f32x4 (&acc)[FM][FN], int wm, int wn, int lane) {
+  constexpr int P = BN + 4;
+  const int g = lane >> 4, r16 = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        tile[(wm * WM + i * 16 + g * 4 + e) * P + wn * WN + j * 16 + r16] = acc[i][j][e];
+}
+
+template <typename TO>
+__device__ __forceinline__ void store4(TO* dst, const float4& v);
+template <>
+__device__ __forceinline__ void store4<float>(float* dst, const float4& v) {
+  *reinterpret_cast<float4*>(dst) = v;
+}
+template <>
+__device__ __forceinline__ void store4<__bf16>(__bf16* dst, const float4& v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 o;
+  o[0] = (__bf16)v.x; o[1] = (__bf16)v.y; o[2] = (__bf16)v.z; o[3] = (__bf16)v.w;
+  *reinterpret_cast<bf16x4*>(dst) = o;
+}
+
+// Requires a __syncthreads() between acc_to_lds and this call (done inside).
+template <typename TO, int BM, int BN>
+__device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0, int n0) {
+  constexpr int P = BN + 4, C4 = BN / 4;
+  const int tid = threadIdx.x;
+  __syncthreads();
+  float amax = 0.f;
+  TO* out = reinterpret_cast<TO*>(p.out);
+  const int HW = p.H * p.W;
+  for (int idx = tid; idx < BM * C4; idx += 256) {
+    const int row = idx / C4, c4 = idx - row * C4;
+    const int m = m0 + row, co = n0 + c4 * 4;
+    if (m >= p.M || co >= p.cout_p) continue;
+    float4 v = *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
+    const float4 b = *reinterpret_cast<const float4*>(p.bias + co);
+    v.x = kpd_act(v.x * p.scale + b.x, p.act);
+    v.y = kpd_act(v.y * p.scale + b.y, p.act);
+    v.z = kpd_act(v.z * p.scale + b.z, p.act);
+    v.w = kpd_act(v.w * p.scale + b.w, p.act);
+    if (p.res) {
+      const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
+      int sy = y, sx = x;
+      if (p.rh != p.H) sy = min((int)floorf((float)y * ((float)p.rh / (float)p.H)), p.rh - 1);
+      if (p.rw != p.W) sx = min((int)floorf((float)x * ((float)p.rw / (float)p.W)), p.rw - 1);
+      const float4 q = *reinterpret_cast<const float4*>(p.res + ((size_t)(n * p.rh + sy) * p.rw + sx) * p.cout_p + co);
+      v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    }
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    store4<TO>(out + (size_t)m * p.out_cstride + co, v);
+    if (p.stats) *reinterpret_cast<float4*>(tile + row * P + c4 * 4) = v;
+  }
+  if (p.amax) {
+    const float w = wave_max(amax);
+    if ((tid & 63) == 0 && w > 0.f) atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(w));
+  }
+  if (p.stats) {
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.cout_p) {
+      float s = 0.f, mx = -INFINITY;
+      for (int r = 0; r < BM; ++r) {
+        const float v = tile[r * P + tid];
+        s += v;
+        mx = fmaxf(mx, v);
+      }
+      const int n = m0 / HW, t = (m0 - n * HW) / BM;
+      float* st = p.stats + ((size_t)n * p.tiles_per_img + t) * 2 * p.cout_p;
+      st[n0 + tid] = s;
+      st[p.cout_p + n0 + tid] = mx;
+    }
+  }
+}

@@ -28,6 +28,7 @@
 //     channel sum/max partials (ChannelAttention pooling), bf16/fp32 stores.
 #include "kpd_common.h"
 #include "kpd_kernels.h"
+#include "conv_epilogue.h"
 
 namespace {
 
@@ -45,7 +46,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   static_assert(FM >= 1 && FN >= 1, "tile too small");
   static_assert(ROWB % 64 == 0, "BK must cover 64 bytes");
 
-  __shared__ __attribute__((aligned(16))) char lds[2 * (BM + BN) * LDSROW];
+  constexpr int MAIN_LDS = 2 * (BM + BN) * LDSROW;
+  constexpr int EPI_LDS = epi_lds_bytes<BM, BN>();
+  __shared__ __attribute__((aligned(16))) char lds[MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS];
   char* As = lds;
   char* Bs = lds + 2 * BM * LDSROW;
 
@@ -173,69 +176,14 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  TO* __restrict__ out = reinterpret_cast<TO*>(p.out);
-  const bool do_stats = p.stats != nullptr;
-  float s_sum[FN], s_max[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) { s_sum[j] = 0.f; s_max[j] = -INFINITY; }
-
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + wm * WM + i * 16 + g * 4 + e;
-      if (m >= M) continue;
-      size_t res_row = 0;
-      if (p.res) {
-        const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
-        int sy = y, sx = x;
-        if (p.rh != H) sy = min((int)floorf((float)y * ((float)p.rh / (float)H)), p.rh - 1);
-        if (p.rw != W) sx = min((int)floorf((float)x * ((float)p.rw / (float)W)), p.rw - 1);
-        res_row = ((size_t)(n * p.rh + sy) * p.rw + sx) * cout_p;
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int co = n0 + wn * WN + j * 16 + r16;
-        if (co >= cout_p) continue;
-        float v = acc[i][j][e] + p.bias[co];
-        v = kpd_act(v, p.act);
-        if (p.res) v += p.res[res_row + co];
-        s_sum[j] += v;
-        s_max[j] = fmaxf(s_max[j], v);
-        out[(size_t)m * p.out_cstride + co] = (TO)v;
-      }
-    }
-  }
-
-  if (do_stats) {
-    // Per-column partials: reduce over the 4 lane groups, then over the 2 M-waves.
-    __syncthreads();  // LDS reuse
-    float* red = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = s_sum[j], mx = s_max[j];
-      s += __shfl_xor(s, 16, 64); mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      s += __shfl_xor(s, 32, 64); mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (g == 0) {
-        const int col = wn * WN + j * 16 + r16;
-        red[(wm * BN + col) * 2 + 0] = s;
-        red[(wm * BN + col) * 2 + 1] = mx;
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const int co = n0 + tid;
-      if (co < cout_p) {
-        const float s = red[(0 * BN + tid) * 2] + red[(1 * BN + tid) * 2];
-        const float mx = fmaxf(red[(0 * BN + tid) * 2 + 1], red[(1 * BN + tid) * 2 + 1]);
-        const int n = m0 / HW, t = (m0 - n * HW) / BM;
-        float* st = p.stats + ((size_t)n * p.tiles_per_img + t) * 2 * cout_p;
-        st[co] = s;
-        st[cout_p + co] = mx;
-      }
-    }
-  }
+  // ---------------- epilogue (LDS-staged, 16-byte row stores) ----------------
+  float* tile = reinterpret_cast<float*>(lds);
+  acc_to_lds<FM, FN, WM, WN, BN>(tile, acc, wm, wn, lane);
+  EpiArgs e;
+  e.bias = p.bias; e.out = p.out; e.res = p.res; e.stats = p.stats; e.amax = p.amax; e.scale = 1.f;
+  e.M = M; e.H = H; e.W = W; e.cout_p = cout_p; e.out_cstride = p.out_cstride; e.rh = p.rh; e.rw = p.rw;
+  e.act = p.act; e.tiles_per_img = p.tiles_per_img;
+  tile_store<TO, BM, BN>(tile, e, m0, n0);
 }
 
 template <typename TA, typename TO, int KS, int BM, int BN, int BK>
@@ -259,6 +207,16 @@ hipError_t launch_conv(const ConvArgs& a, ConvDType dt, int ks, hipStream_t st) 
       return launch<float, float, 3, 128, 128, 32>(a, st);
     }
     if (ks != 1) return hipErrorInvalidValue;
+    // small GEMMs (MobileNet body, coarse FPN laterals): halve the M tile so the
+    // grid covers the 256 CUs at least twice
+    const long blocks128 = (long)((a.M + 127) / 128) * ((a.cout_p + 127) / 128);
+    if (blocks128 < 512 && a.stats == nullptr) {
+      if (a.cout_p <= 32) return bk32 ? launch<float, float, 1, 64, 32, 32>(a, st)
+                                      : launch<float, float, 1, 64, 32, 16>(a, st);
+      if (a.cout_p <= 64) return bk32 ? launch<float, float, 1, 64, 64, 32>(a, st)
+                                      : launch<float, float, 1, 64, 64, 16>(a, st);
+      return bk32 ? launch<float, float, 1, 64, 128, 32>(a, st) : launch<float, float, 1, 64, 128, 16>(a, st);
+    }
     if (a.cout_p <= 32) return bk32 ? launch<float, float, 1, 128, 32, 32>(a, st)
                                     : launch<float, float, 1, 128, 32, 16>(a, st);
     if (a.cout_p <= 64) return bk32 ? launch<float, float, 1, 128, 64, 32>(a, st)

@@ -287,30 +287,43 @@ __global__ __launch_bounds__(64) void hm_final_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- decode
-// grid R, 256 threads (4 waves, each takes keypoints k = wave, wave+4, ...).
-__global__ __launch_bounds__(256) void decode_kernel(const float* __restrict__ heat_out,
-                                                     const float* __restrict__ boxes,
-                                                     const int32_t* __restrict__ slot, int P,
-                                                     float* __restrict__ kpts_out, float* __restrict__ vis_out) {
-  const int r = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// grid (R, 17), one wave per (roi, keypoint); single pass over the 3136
+// heatmap values with an online (running-max) softmax per lane, lanes then
+// merged pairwise -- the heatmap is read once.
+__global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ heat_out,
+                                                    const float* __restrict__ boxes,
+                                                    const int32_t* __restrict__ slot, int P,
+                                                    float* __restrict__ kpts_out, float* __restrict__ vis_out) {
+  const int r = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
   const int sl = slot[r];
   if (sl < 0) return;
   const int bimg = r / P;
   const size_t o = (size_t)(bimg * P + sl) * NK;
   const float cx = boxes[r * 4 + 0], cy = boxes[r * 4 + 1], bw = boxes[r * 4 + 2], bh = boxes[r * 4 + 3];
-  for (int k = wave; k < NK; k += 4) {
+  {
     const float* hp = heat_out + (o + k) * HMP;
-    float m = -INFINITY;
-    for (int i = lane; i < HMP; i += 64) m = fmaxf(m, hp[i]);
-    m = wave_max(m);
-    float se = 0.f, sx = 0.f, sy = 0.f;
+    float m = -INFINITY, se = 0.f, sx = 0.f, sy = 0.f;
     for (int i = lane; i < HMP; i += 64) {
-      const float e = expf(hp[i] - m);
+      const float h = hp[i];
+      if (h > m) {  // rescale running sums to the new max
+        const float c = expf(m - h);
+        se *= c; sx *= c; sy *= c;
+        m = h;
+      }
+      const float e = expf(h - m);
       se += e;
       sx = fmaf(e, (float)(i % HM), sx);
       sy = fmaf(e, (float)(i / HM), sy);
     }
-    se = wave_sum(se); sx = wave_sum(sx); sy = wave_sum(sy);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float m2 = __shfl_xor(m, off, 64);
+      const float se2 = __shfl_xor(se, off, 64), sx2 = __shfl_xor(sx, off, 64), sy2 = __shfl_xor(sy, off, 64);
+      const float mn = fmaxf(m, m2);
+      const float c1 = expf(m - mn), c2 = expf(m2 - mn);
+      se = se * c1 + se2 * c2; sx = sx * c1 + sx2 * c2; sy = sy * c1 + sy2 * c2;
+      m = mn;
+    }
     if (lane == 0) {
       const float kx = (sx / se) / (float)(HM - 1);
       const float ky = (sy / se) / (float)(HM - 1);
@@ -365,6 +378,6 @@ hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* 
 }
 hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_t* slot, int R, int P,
                          float* kpts_out, float* vis_out, hipStream_t st) {
-  hipLaunchKernelGGL(decode_kernel, dim3(R), dim3(256), 0, st, heat_out, boxes, slot, P, kpts_out, vis_out);
+  hipLaunchKernelGGL(decode_kernel, dim3(R, NK), dim3(64), 0, st, heat_out, boxes, slot, P, kpts_out, vis_out);
   return hipGetLastError();
 }

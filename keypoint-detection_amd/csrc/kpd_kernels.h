@@ -18,7 +18,21 @@ struct ConvArgs {
   int act;
   int M;                 // N*H*W
   int tiles_per_img;
+  float* amax;           // optional: atomicMax of |out| (float bits; caller zeroes it)
 };
+
+// FPN level-0 3x3 conv on the f16 MFMA pipe with hi/lo operand split (conv_split16.hip)
+struct Split16Args {
+  const float* in;       // NHWC [N][H][W][cin] f32 (lateral 0)
+  const _Float16* w_hi;  // [cout_p][9][cin], BN-folded, scaled by 2^w_exp
+  const _Float16* w_lo;
+  const float* bias;     // [cout_p]
+  float* out;            // NHWC [N][H][W][cout_p]
+  float* stats;          // [N][tiles_per_img][2][cout_p] or null
+  const float* amax;     // device max|in| (published by the lateral conv)
+  int N, H, W, cin, cout_p, act, M, tiles_per_img, w_exp;
+};
+hipError_t launch_conv3x3_split16(const Split16Args& a, hipStream_t st);
 
 enum ConvDType : int { CONV_F32 = 0, CONV_BF16_OUT_BF16 = 1, CONV_BF16_OUT_F32 = 2 };
 

@@ -110,6 +110,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   void* h2 = nullptr;
   float* h3 = nullptr;
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
+  float* amax = nullptr;  // max|lateral0| for the split16 FPN conv scale
 };
 
 struct Dims {
@@ -141,6 +142,7 @@ struct kpd_plan {
   float *hca_w0 = nullptr, *hca_b0 = nullptr, *hca_w2 = nullptr, *hca_b2 = nullptr;
   float *sa_w = nullptr, *sa_b = nullptr;
   DevConv hm1, hm2, hm3;
+  struct { _Float16 *hi = nullptr, *lo = nullptr; int w_exp = 0; } fpn0s;  // split16 weights
   float *fin_w = nullptr, *fin_b = nullptr;
   float* zero_bias = nullptr;  // 128 zeros for bias-free laterals
   // workspace
@@ -265,6 +267,29 @@ int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& m
   return upload(p, w->data, out);
 }
 
+// Split16 weights for the FPN level-0 conv: downloads the packed fp32 weights
+// [cout_p][9][cin_p], scales by 2^w_exp so max|w| < 2^15, splits into f16 hi/lo.
+int pack_split16(kpd_plan* p, const DevConv& dc) {
+  const size_t n = (size_t)dc.cout_p * 9 * dc.cin_p;
+  std::vector<float> w(n);
+  HIP_TRY(hipMemcpy(w.data(), dc.w, n * sizeof(float), hipMemcpyDeviceToHost));
+  float mx = 0.f;
+  for (float v : w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) std::frexp(mx, &e);
+  const int w_exp = std::min(std::max(14 - e, -100), 100);
+  std::vector<_Float16> hi(n), lo(n);
+  for (size_t i = 0; i < n; ++i) {
+    const float x = std::ldexp(w[i], w_exp);
+    hi[i] = (_Float16)x;
+    lo[i] = (_Float16)(x - (float)hi[i]);
+  }
+  if (int rc = upload(p, hi, &p->fpn0s.hi)) return rc;
+  if (int rc = upload(p, lo, &p->fpn0s.lo)) return rc;
+  p->fpn0s.w_exp = w_exp;
+  return KPD_OK;
+}
+
 // ------------------------------------------------------------------ workspace
 struct Carver {
   char* base;
@@ -296,6 +321,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   for (int i = 0; i < 4; ++i) w.lat[i] = c.take<float>((size_t)B * lh[i] * lw[i] * 128);
   w.feat = c.take<float>((size_t)B * d.Hf * d.Wf * 128);
   w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
+  w.amax = c.take<float>(1);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
@@ -340,8 +366,9 @@ struct Stage {
 
 int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, void* out, int act,
          const float* res, int rh, int rw, const float* a_scale, float* stats, int tiles, int out_kind,
-         hipStream_t st) {
+         hipStream_t st, float* amax = nullptr) {
   ConvArgs a{};
+  a.amax = amax;
   a.in = in; a.wt = L.w; a.bias = L.b; a.out = out; a.res = res; a.a_scale = a_scale; a.stats = stats;
   a.N = N; a.H = H; a.W = W; a.cin_p = L.cin_p; a.cout_p = L.cout_p;
   a.in_cstride = in_cstride; a.out_cstride = L.cout_p;
@@ -403,6 +430,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   HIP_TRY(hipSetDevice(p->device));
   for (void* a : p->allocs) (void)hipFree(a);
   p->allocs.clear();
+  p->fpn0s.hi = p->fpn0s.lo = nullptr;
   if (p->ws) { (void)hipFree(p->ws); p->ws = nullptr; p->ws_bytes = 0; }
   p->have_work = false;
   p->precision = precision;
@@ -462,6 +490,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
+  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_split16(p, p->fpn0));
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
@@ -575,19 +604,30 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, con
 
   // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
   const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
+  const bool split = p->precision == KPD_PRECISION_MIXED && p->fpn0s.hi != nullptr;
   std::unique_ptr<Stage> lat_stage(new Stage(p, "fpn_lateral", st));
   for (int i = 3; i >= 0; --i) {
     const DevConv& L = p->lat[i];
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
+    if (i == 0 && split) HIP_TRY(hipMemsetAsync(w.amax, 0, sizeof(float), st));
     if (int rc = conv(L, taps[i], B, lh[i], lw[i], pad16(kFpnIn[i]), w.lat[i], ACT_NONE, res,
-                      i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st))
+                      i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st,
+                      (i == 0 && split) ? w.amax : nullptr))
       return rc;
   }
   lat_stage.reset();
   std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
-  if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
-                    d.fused_stats ? w.stats : nullptr, d.tiles, 0, st))
+  if (split) {
+    Split16Args sa{};
+    sa.in = w.lat[0]; sa.w_hi = p->fpn0s.hi; sa.w_lo = p->fpn0s.lo; sa.bias = p->fpn0.b; sa.out = w.feat;
+    sa.stats = d.fused_stats ? w.stats : nullptr; sa.amax = w.amax;
+    sa.N = B; sa.H = d.Hf; sa.W = d.Wf; sa.cin = 128; sa.cout_p = 128; sa.act = ACT_RELU; sa.M = B * HWf;
+    sa.tiles_per_img = d.tiles; sa.w_exp = p->fpn0s.w_exp;
+    HIP_TRY(launch_conv3x3_split16(sa, st));
+  } else if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
+                           d.fused_stats ? w.stats : nullptr, d.tiles, 0, st)) {
     return rc;
+  }
   fpn_stage.reset();
   std::unique_ptr<Stage> topk_stage(new Stage(p, "topk", st));
   if (!d.fused_stats) HIP_TRY(launch_channel_stats(w.feat, B, HWf, 128, d.tiles, w.stats, st));

@@ -13,8 +13,9 @@ import os
 import sys
 from collections import defaultdict
 
-STAGE_OF = {
-    "conv_mfma_kernel<float, float, 3, 128, 128, 32>": "fpn0",
+STAGE_OF = {   # kernel-name substring -> "<stage>:<bench precision>"
+    "conv_mfma_kernel<float, float, 3, 128, 128, 32>": "fpn0:fp32",
+    "conv3x3_split16_kernel": "fpn0:mixed",
 }
 
 
