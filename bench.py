@@ -132,17 +132,14 @@ def main():
     batch = {"image": img, "bboxes": boxes}
     plan = m.native_plan(dev)
 
-    gather_bufs = None
-    if dist and not a.no_gather:
-        import torch.distributed as tdist
-        gather_bufs = ([torch.empty(B, P, 1, 17, 2, device=dev) for _ in range(world)],
-                       [torch.empty(B, P, 1, 17, 3, device=dev) for _ in range(world)])
+    gather = dist and not a.no_gather
+    if gather:
+        from dll.distributed import collate_outputs
 
     def step():
         out = m(batch)
-        if gather_bufs is not None:
-            tdist.all_gather(gather_bufs[0], out["keypoints"])
-            tdist.all_gather(gather_bufs[1], out["visibilities"])
+        if gather:   # result collation over RCCL: P all_reduce(MAX) + kpt/vis all_gather
+            collate_outputs(out, B * world)
         return out
 
     with torch.no_grad():
@@ -214,7 +211,7 @@ def main():
                    "model": "MultiPersonKeypointModel (MobileNetV3-Small+FPN, HeatmapHead)",
                    "global_batch": B * world, "height": a.height, "width": a.width, "persons": P,
                    "precision": a.precision, "parallelism": f"dp{world}",
-                   "gather": bool(gather_bufs is not None)},
+                   "gather": bool(gather)},
         "gflop_per_image": round(fl["total"] / 1e9, 3),
         "achieved_tflops_total": round(fl["total"] * total_imgs / el / 1e12, 2),
         "roofline": roof,

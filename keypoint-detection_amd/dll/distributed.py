@@ -1,0 +1,83 @@
+"""One-process-per-GPU data parallelism for the inference path.
+
+Images are independent in eval (BN running stats, dropout off, per-image box
+loops -- reference keypoint_model.py:143-199), so a global batch shards into
+contiguous image ranges with no exchange in the data path.  The only
+collectives are the result collation the serving path needs:
+  * all_reduce(MAX) of the per-rank padded person count P (outputs are padded
+    to the global max, reference :138,181-183);
+  * all_gather of the fixed-size per-image keypoint / visibility slabs
+    (340 B per person) -- tiny, latency-bound messages over RCCL/xGMI.
+Heatmaps (213 KB per person) stay sharded unless asked for.
+Works with any torch.distributed backend ("nccl" = RCCL on ROCm; "gloo" for
+the CPU tests).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous [start, stop) image range of ``rank``; the first total % world
+    ranks take one extra image."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def global_max_persons(p_local: int, device, group=None) -> int:
+    t = torch.tensor([p_local], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def pad_persons(x: torch.Tensor, p: int) -> torch.Tensor:
+    """Zero-pad dim 1 (persons) to ``p`` (reference pad_to_length semantics)."""
+    if x.size(1) == p:
+        return x
+    pad = torch.zeros((x.size(0), p - x.size(1)) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
+    return torch.cat([x, pad], dim=1)
+
+
+def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
+    """all_gather a per-image tensor [n_local, ...] sharded by ``shard_range``
+    into [total, ...] on every rank (uneven shards padded then trimmed)."""
+    world = dist.get_world_size(group)
+    counts = [shard_range(total, world, r) for r in range(world)]
+    mx = max(b - a for a, b in counts)
+    buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    buf[: local.size(0)] = local
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
+
+
+def collate_outputs(out: Dict[str, torch.Tensor], total: int, group=None,
+                    keys: Sequence[str] = ("keypoints", "visibilities")) -> Dict[str, torch.Tensor]:
+    """Pad this rank's outputs to the global person count and all-gather ``keys``."""
+    p = global_max_persons(out["keypoints"].size(1), out["keypoints"].device, group)
+    res = {}
+    for k in keys:
+        res[k] = gather_images(pad_persons(out[k], p), total, group)
+    return res
+
+
+def sharded_forward(model, images: torch.Tensor, boxes: torch.Tensor, group=None,
+                    keys: Sequence[str] = ("keypoints", "visibilities")) -> Dict[str, torch.Tensor]:
+    """Run this rank's shard of a global batch and return the collated outputs
+    of the whole batch on every rank."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = shard_range(images.size(0), world, rank)
+    if b > a:
+        out = model({"image": images[a:b], "bboxes": boxes[a:b]})
+    else:   # more ranks than images: contribute an empty shard
+        k = getattr(model, "num_keypoints", 17)
+        out = {"keypoints": torch.zeros(0, 0, 1, k, 2, device=images.device),
+               "visibilities": torch.zeros(0, 0, 1, k, 3, device=images.device)}
+    return collate_outputs(out, images.size(0), group, keys)

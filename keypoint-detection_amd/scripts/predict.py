@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Keypoint prediction CLI -- same flags and printout as the reference
+(scripts/predict.py:162-223, print format :118-129), with working imports.
+
+    python scripts/predict.py --config configs/default_config.yaml \
+        --model best_model.pth --input img.jpg --gt img.txt --output out/
+
+Differences (documented in DESIGN.md):
+  * the reference's ITransform needs OpenCV (CLAHE + Canny blend), absent in
+    this image; the image is resized/normalised like ITransform's torchvision
+    tail (Resize, ToTensor, Normalize) without the cv2 stage;
+  * ``--model synthetic`` builds the seeded synthetic weights (no trained
+    checkpoint exists: the reference's outputs/best_model.pth is a missing blob);
+  * ``--size HxW`` allows the non-square 256x192 input of BASELINE config C1.
+Runs on the HIP device (the accelerated path has no CPU fallback).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from dll.configs import (BackboneConfig, KeypointHeadConfig, ModelConfig,  # noqa: E402
+                         PersonDetectionConfig, TrainingConfig)
+from dll.models import MultiPersonKeypointModel  # noqa: E402
+
+KEYPOINT_NAMES = ["nose", "left_eye", "right_eye", "left_ear", "right_ear", "left_shoulder", "right_shoulder",
+                  "left_elbow", "right_elbow", "left_wrist", "right_wrist", "left_hip", "right_hip", "left_knee",
+                  "right_knee", "left_ankle", "right_ankle"]
+
+
+def load_config(path):
+    import yaml
+    with open(path) as f:
+        return yaml.safe_load(f)
+
+
+def setup_logging():
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
+
+
+def load_model(model_path, config_dict, device, precision="fp32"):
+    """Reference load_model (:30-62): configs from the YAML, filtered
+    strict=False state-dict load (weights_only -- nothing executable is
+    unpickled)."""
+    mc = config_dict["model"]
+    model_config = ModelConfig(backbone=BackboneConfig(**mc["backbone"]),
+                               person_head=PersonDetectionConfig(**mc["person_head"]),
+                               keypoint_head=KeypointHeadConfig(**mc["keypoint_head"]),
+                               num_keypoints=mc["keypoint_head"]["num_keypoints"])
+    model = MultiPersonKeypointModel(model_config, TrainingConfig(), precision=precision)
+    if str(model_path) == "synthetic":
+        from dll.models.synthetic import synthetic_state_dict
+        model.load_state_dict(synthetic_state_dict(model.state_dict(), seed=0))
+    else:
+        ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
+        sd = ckpt["model_state_dict"] if isinstance(ckpt, dict) and "model_state_dict" in ckpt else ckpt
+        own = model.state_dict()
+        model.load_state_dict({k: v for k, v in sd.items() if k in own}, strict=False)
+    return model.to(device).eval()
+
+
+def make_transform(in_channels: int, size):
+    """Resize -> ToTensor -> Normalize (ITransform without its cv2 stage)."""
+    h, w = size
+
+    def tf(img):
+        import numpy as np
+        img = img.convert("L" if in_channels == 1 else "RGB").resize((w, h), resample=2)  # bilinear
+        x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0)
+        x = x[None] if x.dim() == 2 else x.permute(2, 0, 1)
+        if in_channels == 1:
+            return (x - 0.5) / 0.5
+        m = torch.tensor([0.485, 0.456, 0.406]).view(3, 1, 1)
+        s = torch.tensor([0.229, 0.224, 0.225]).view(3, 1, 1)
+        return (x - m) / s
+    return tf
+
+
+def read_gt_boxes(gt_path, device):
+    """YOLO label lines 'cls cx cy w h ...' -> [P,4] (reference :78-93)."""
+    boxes = []
+    with open(gt_path) as f:
+        for line in f:
+            d = line.strip().split()
+            if len(d) >= 5:
+                boxes.append([float(d[1]), float(d[2]), float(d[3]), float(d[4])])
+    return torch.tensor(boxes, device=device)
+
+
+def predict_single_image(model, image_path, transform, device, gt_path=None, output_path=None):
+    from PIL import Image
+    x = transform(Image.open(image_path)).unsqueeze(0).to(device)
+    bboxes = read_gt_boxes(gt_path, device) if gt_path and Path(gt_path).exists() else None
+    with torch.no_grad():
+        outputs = model({"image": x, "bboxes": bboxes.unsqueeze(0) if bboxes is not None else None})
+    keypoints = outputs["keypoints"].squeeze().cpu().numpy()
+    print("\nPredicted Keypoints:")
+    print("-" * 40)
+    print(f"Keypoints shape: {keypoints.shape}")
+    if len(keypoints.shape) == 3:
+        keypoints = keypoints[0]
+    for i, name in enumerate(KEYPOINT_NAMES):
+        if i < len(keypoints):
+            x_, y_ = keypoints[i]
+            print(f"{i + 1:2d}. {name:<15} ({x_:.3f}, {y_:.3f})")
+    return keypoints
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Predict keypoints in images")
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--model", required=True, help="checkpoint path, or 'synthetic'")
+    ap.add_argument("--input", required=True)
+    ap.add_argument("--gt")
+    ap.add_argument("--output", required=True)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "mixed"])
+    ap.add_argument("--size", default=None, help="HxW input size (default: input_size square)")
+    args = ap.parse_args(argv)
+    setup_logging()
+    cfg = load_config(args.config)
+    device = torch.device(args.device)
+    bcfg = cfg["model"]["backbone"]
+    size = tuple(int(v) for v in args.size.split("x")) if args.size else (bcfg["input_size"], bcfg["input_size"])
+    transform = make_transform(bcfg.get("in_channels", 3), size)
+    logging.info(f"Loading model from {args.model}")
+    model = load_model(args.model, cfg, device, args.precision)
+    inp = Path(args.input)
+    gt = Path(args.gt) if args.gt else None
+    Path(args.output).mkdir(parents=True, exist_ok=True)
+    if inp.is_file():
+        predict_single_image(model, inp, transform, device, gt if gt and gt.is_file() else None)
+    else:
+        for img in sorted(inp.glob("*.*")):
+            if img.suffix.lower() in (".jpg", ".jpeg", ".png"):
+                predict_single_image(model, img, transform, device, (gt / f"{img.stem}.txt") if gt else None)
+    logging.info("Prediction completed successfully!")
+
+
+if __name__ == "__main__":
+    main()

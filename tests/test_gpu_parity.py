@@ -190,3 +190,22 @@ def test_nms_gpu_vs_golden(golden_dir):
             assert [sc[k] for k in keep] == [sc[k] for k in ref], f"case {i}"
             assert sorted(keep) == sorted(ref), f"case {i}"
         i += 1
+
+
+def test_predict_cli(tmp_path, capsys):
+    """scripts/predict.py end to end: YAML config (grayscale 224), synthetic
+    weights, a PNG and a YOLO label; printout format of the reference."""
+    import sys
+    from PIL import Image
+    from conftest import PKG
+    sys.path.insert(0, str(PKG / "scripts"))
+    import predict
+    rng = np.random.default_rng(0)
+    Image.fromarray(rng.integers(0, 255, (240, 180, 3), dtype=np.uint8)).save(tmp_path / "img.png")
+    (tmp_path / "img.txt").write_text("0 0.5 0.5 0.4 0.8\n0 0.3 0.4 0.2 0.3\n")
+    predict.main(["--config", str(PKG / "configs" / "default_config.yaml"), "--model", "synthetic",
+                  "--input", str(tmp_path / "img.png"), "--gt", str(tmp_path / "img.txt"),
+                  "--output", str(tmp_path / "out")])
+    txt = capsys.readouterr().out
+    assert "Keypoints shape: (2, 17, 2)" in txt
+    assert " 1. nose" in txt and "17. right_ankle" in txt
