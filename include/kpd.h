@@ -62,21 +62,35 @@ int kpd_plan_finalize(kpd_plan* plan, int precision);
 
 void kpd_plan_destroy(kpd_plan* plan);
 
-/* Full eval forward with given boxes.
+#define KPD_FLAG_DETECT 1     /* no caller boxes: person detector + NMS WRITE boxes [B][P][4] */
+#define KPD_FLAG_DUAL_HEAD 2  /* also run KEYPOINT_HEAD on 128-ch ROI features */
+
+/* Full eval forward.
  *   image:  [B][C][H][W] fp32 (NCHW, as the reference receives it), device
  *   boxes:  [nbox_images][P][4] fp32 cxcywh normalised to [0,1], device;
- *           nbox_images <= B (the reference iterates over the box list)
+ *           nbox_images <= B (the reference iterates over the box list).
+ *           With KPD_FLAG_DETECT it is an OUTPUT (nbox_images == B, P = max
+ *           persons kept per image, zero padded) -- build-defined glue for
+ *           the reference's person-detector branch.
  *   keypoints:    [nbox_images][P][1][17][2]  fp32 out
  *   visibilities: [nbox_images][P][1][17][3]  fp32 out (one-hot 3-class)
  *   heatmap:      [nbox_images][P][17][56][56] fp32 out, may be NULL
+ *   kh_keypoints / kh_visibilities: [nbox_images][P][1][17][2|3] sigmoid
+ *                 outputs of KEYPOINT_HEAD (KPD_FLAG_DUAL_HEAD), else NULL
+ *   box_scores:   [B][P] detector scores (KPD_FLAG_DETECT), may be NULL
  *   topk_out:     [B][64] int32 channel indices, may be NULL (debug)
  * All-zero boxes are skipped and the remaining persons compacted, images
  * without a valid box get the reference's dummy person, P is kept as the
  * padded person count -- exactly keypoint_model.py:138-206. */
 int kpd_forward(kpd_plan* plan, const float* image, int B, int C, int H, int W,
-                const float* boxes, int nbox_images, int P,
+                float* boxes, int nbox_images, int P, int flags,
                 float* keypoints, float* visibilities, float* heatmap,
+                float* kh_keypoints, float* kh_visibilities, float* box_scores,
                 int32_t* topk_out, void* stream);
+
+/* Detector thresholds (PersonDetectionConfig.conf_threshold /
+ * nms_iou_threshold, model_config.py:27-28); defaults 0.3 / 0.3. */
+int kpd_plan_set_detector(kpd_plan* plan, float conf_threshold, float nms_iou_threshold);
 
 /* Copy an internal buffer recorded by the last kpd_forward into `dst`
  * (device memory, `bytes` long).  Names: "feat0" ([B][Hf][Wf][128] NHWC f32),

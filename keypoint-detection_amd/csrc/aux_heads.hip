@@ -1,0 +1,194 @@
+// Person-detector glue and KEYPOINT_HEAD ("dual head") kernels (gfx950).
+//
+// Person detector (reference PERSON_HEAD, dll/models/person_head.py:7-166; the
+// reference never decodes or NMSes inside forward, so the glue is
+// build-defined -- DESIGN.md §C3, oracle.kpd_oracle.person_detect):
+//   pool:   FPN level 0 adaptive-avg-pooled to the 56x56 anchor grid
+//   heads:  box_heads[0] / cls_heads[0] as one 1x1 MFMA conv (conv_mfma.hip)
+//   decode: sigmoid score, threshold, anchor decode (this file)
+//   NMS:    nms.hip, one workgroup per image, max_persons kept, zero padded
+//
+// KEYPOINT_HEAD (dll/models/keypoint_head.py:9-90) on the 128-channel ROI
+// features: spatial attention apply (this file), ResidualBlocks and 3x3 convs
+// on the MFMA conv kernel (post-affine epilogue for ResidualBlock.bn1),
+// adaptive pools (this file), the two Linear layers as MFMA GEMMs, and
+// LayerNorm + ReLU6 + Linear + sigmoid tails (this file).
+#include "kpd_common.h"
+#include "kpd_kernels.h"
+
+namespace {
+constexpr int G = 56, GP = G * G, NA = 9;
+
+// [B][Hf][Wf][C] -> [B][56][56][C], PyTorch adaptive_avg_pool2d bins; thread per (cell, channel quad)
+__global__ __launch_bounds__(256) void adaptive_pool56_kernel(const float* __restrict__ in, int B, int Hf, int Wf,
+                                                              int C, float* __restrict__ out) {
+  const int nq = C / 4;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)B * GP * nq) return;
+  const int q = idx % nq;
+  const size_t cell = idx / nq;
+  const int b = cell / GP, r = cell - (size_t)b * GP, i = r / G, j = r - i * G;
+  const int y0 = (i * Hf) / G, y1 = ((i + 1) * Hf + G - 1) / G;
+  const int x0 = (j * Wf) / G, x1 = ((j + 1) * Wf + G - 1) / G;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int y = y0; y < y1; ++y)
+    for (int x = x0; x < x1; ++x) {
+      const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)b * Hf + y) * Wf + x) * C + q * 4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  const float cnt = (float)((y1 - y0) * (x1 - x0));
+  *reinterpret_cast<float4*>(out + cell * C + q * 4) = make_float4(s.x / cnt, s.y / cnt, s.z / cnt, s.w / cnt);
+}
+
+// head output [B][56*56][hc] (channels 0..35 box deltas (anchor a, coord c at a*4+c), 36..44 logits)
+// -> candidates [B][56*56*9][4] boxes, [B][..] scores (-inf when <= conf)
+__global__ __launch_bounds__(256) void person_decode_kernel(const float* __restrict__ head, int B, int hc,
+                                                            const float* __restrict__ anchors, float inv_w,
+                                                            float inv_h, float conf, float* __restrict__ cand_boxes,
+                                                            float* __restrict__ cand_scores) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)B * GP * NA) return;
+  const int a = idx % NA;
+  const size_t cell = idx / NA;             // b*GP + (i*56+j)
+  const int anc = (int)(cell % GP) * NA + a;
+  const float* h = head + cell * hc;
+  const float logit = h[36 + a];
+  const float score = kpd_sigmoid(logit);
+  const float ax = anchors[anc * 4 + 0], ay = anchors[anc * 4 + 1];
+  const float aw = anchors[anc * 4 + 2] * inv_w, ah = anchors[anc * 4 + 3] * inv_h;
+  const float clip = 4.135166556742356f;   // log(1000/16)
+  const float cx = ax + h[a * 4 + 0] * aw;
+  const float cy = ay + h[a * 4 + 1] * ah;
+  const float w = aw * expf(fminf(h[a * 4 + 2], clip));
+  const float hh = ah * expf(fminf(h[a * 4 + 3], clip));
+  *reinterpret_cast<float4*>(cand_boxes + idx * 4) = make_float4(cx, cy, w, hh);
+  cand_scores[idx] = score > conf ? score : -INFINITY;
+}
+
+// x'[c] = x[c] * sigmoid(b + sum_k w[k] * sa1[k]) in place; thread per pixel.
+__global__ __launch_bounds__(256) void kh_att_kernel(float* __restrict__ x, const float* __restrict__ sa1,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     size_t npix) {
+  __shared__ float sw[64];
+  if (threadIdx.x < 64) sw[threadIdx.x] = w[threadIdx.x];
+  __syncthreads();
+  const size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= npix) return;
+  const float4* s = reinterpret_cast<const float4*>(sa1 + pix * 64);
+  float a = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 v = s[q];
+    a = fmaf(sw[4 * q], v.x, a); a = fmaf(sw[4 * q + 1], v.y, a);
+    a = fmaf(sw[4 * q + 2], v.z, a); a = fmaf(sw[4 * q + 3], v.w, a);
+  }
+  const float att = kpd_sigmoid(a + b[0]);
+  float4* xp = reinterpret_cast<float4*>(x + pix * 128);
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    float4 v = xp[q];
+    v.x *= att; v.y *= att; v.z *= att; v.w *= att;
+    xp[q] = v;
+  }
+}
+
+// adaptive avg pool of an NHWC [R][56][56][C] map to (o x o), written in
+// NCHW-flatten order (c*o*o + y*o + x) as nn.Flatten after the pool does.
+// grid R, 256 threads over (c, y, x) outputs.
+__global__ __launch_bounds__(256) void kh_pool_kernel(const float* __restrict__ in, int C, int o,
+                                                      float* __restrict__ out, int out_stride) {
+  const int r = blockIdx.x;
+  const int n = C * o * o;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const int c = t / (o * o), rem = t - c * o * o, i = rem / o, j = rem - i * o;
+    const int y0 = (i * G) / o, y1 = ((i + 1) * G + o - 1) / o;
+    const int x0 = (j * G) / o, x1 = ((j + 1) * G + o - 1) / o;
+    float s = 0.f;
+    for (int y = y0; y < y1; ++y)
+      for (int x = x0; x < x1; ++x) s += in[(((size_t)r * G + y) * G + x) * C + c];
+    out[(size_t)r * out_stride + t] = s / (float)((y1 - y0) * (x1 - x0));
+  }
+}
+
+// LayerNorm(n) (eps 1e-5, biased variance) + ReLU6 + Linear(n -> m) + sigmoid for one ROI.
+__device__ void ln_linear_sigmoid(const float* __restrict__ y, int n, const float* __restrict__ g,
+                                  const float* __restrict__ bb, const float* __restrict__ w,
+                                  const float* __restrict__ b, int m, float* __restrict__ dst, float* sh) {
+  const int tid = threadIdx.x;
+  __shared__ float red[2][4];
+  float s = 0.f;
+  for (int i = tid; i < n; i += 256) s += y[i];
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[0][tid >> 6] = s;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / (float)n;
+  float v = 0.f;
+  for (int i = tid; i < n; i += 256) { const float d = y[i] - mean; v += d * d; }
+  v = wave_sum(v);
+  if ((tid & 63) == 0) red[1][tid >> 6] = v;
+  __syncthreads();
+  const float var = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)n;
+  const float inv = 1.f / sqrtf(var + 1e-5f);
+  for (int i = tid; i < n; i += 256) sh[i] = fminf(fmaxf((y[i] - mean) * inv * g[i] + bb[i], 0.f), 6.f);
+  __syncthreads();
+  for (int k = tid; k < m; k += 256) {
+    float a = b[k];
+    for (int i = 0; i < n; ++i) a = fmaf(w[k * n + i], sh[i], a);
+    dst[k] = kpd_sigmoid(a);
+  }
+  __syncthreads();
+}
+
+// grid R.  lin_r [R][256] (regression Linear out), lin_v [R][128] (visibility).
+__global__ __launch_bounds__(256) void kh_final_kernel(const float* __restrict__ lin_r, int r_stride,
+                                                       const float* __restrict__ lin_v, int v_stride,
+                                                       const float* ln_rg, const float* ln_rb, const float* w_r,
+                                                       const float* b_r, const float* ln_vg, const float* ln_vb,
+                                                       const float* w_v, const float* b_v,
+                                                       const int32_t* __restrict__ slot, int P,
+                                                       float* __restrict__ kh_kpts, float* __restrict__ kh_vis) {
+  __shared__ float sh[256];
+  const int r = blockIdx.x;
+  const int sl = slot[r];
+  if (sl < 0) return;
+  const size_t o = (size_t)((r / P) * P + sl) * 17;
+  ln_linear_sigmoid(lin_r + (size_t)r * r_stride, 256, ln_rg, ln_rb, w_r, b_r, 34, kh_kpts + o * 2, sh);
+  ln_linear_sigmoid(lin_v + (size_t)r * v_stride, 128, ln_vg, ln_vb, w_v, b_v, 51, kh_vis + o * 3, sh);
+}
+
+}  // namespace
+
+hipError_t launch_adaptive_pool56(const float* in, int B, int Hf, int Wf, int C, float* out, hipStream_t st) {
+  if (C % 4) return hipErrorInvalidValue;
+  const size_t total = (size_t)B * GP * (C / 4);
+  hipLaunchKernelGGL(adaptive_pool56_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, B, Hf, Wf,
+                     C, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_person_decode(const float* head, int B, int hc, const float* anchors, int img_h, int img_w,
+                                float conf, float* cand_boxes, float* cand_scores, hipStream_t st) {
+  const size_t total = (size_t)B * GP * NA;
+  hipLaunchKernelGGL(person_decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, head, B, hc,
+                     anchors, 1.f / (float)img_w, 1.f / (float)img_h, conf, cand_boxes, cand_scores);
+  return hipGetLastError();
+}
+
+hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st) {
+  hipLaunchKernelGGL(kh_att_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, x, sa1, w, b, npix);
+  return hipGetLastError();
+}
+
+hipError_t launch_kh_pool(const float* in, int R, int C, int o, float* out, int out_stride, hipStream_t st) {
+  hipLaunchKernelGGL(kh_pool_kernel, dim3(R), dim3(256), 0, st, in, C, o, out, out_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_kh_final(const float* lin_r, int r_stride, const float* lin_v, int v_stride, const float* ln_rg,
+                           const float* ln_rb, const float* w_r, const float* b_r, const float* ln_vg,
+                           const float* ln_vb, const float* w_v, const float* b_v, const int32_t* slot, int R, int P,
+                           float* kh_kpts, float* kh_vis, hipStream_t st) {
+  hipLaunchKernelGGL(kh_final_kernel, dim3(R), dim3(256), 0, st, lin_r, r_stride, lin_v, v_stride, ln_rg, ln_rb, w_r,
+                     b_r, ln_vg, ln_vb, w_v, b_v, slot, P, kh_kpts, kh_vis);
+  return hipGetLastError();
+}

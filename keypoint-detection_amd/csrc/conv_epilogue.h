@@ -14,6 +14,13 @@ struct EpiArgs {
   float* amax;         // optional atomicMax of |out|
   float scale;         // acc multiplier before bias (split16 unscale), 1 otherwise
   int M, H, W, cout_p, out_cstride, rh, rw, act, tiles_per_img;
+  // optional second per-channel affine after the activation (an un-foldable BN
+  // behind a non-linearity, KEYPOINT_HEAD ResidualBlock.bn1) and its act,
+  // then the residual, then a final activation:
+  //   v = act3( act2( act(acc*scale + bias) * post_scale + post_shift ) + res )
+  const float* post_scale;
+  const float* post_shift;
+  int act2, act3;
 };
 
 template <int BM, int BN>
@@ -66,6 +73,12 @@ __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0
     v.y = kpd_act(v.y * p.scale + b.y, p.act);
     v.z = kpd_act(v.z * p.scale + b.z, p.act);
     v.w = kpd_act(v.w * p.scale + b.w, p.act);
+    if (p.post_scale) {
+      const float4 s = *reinterpret_cast<const float4*>(p.post_scale + co);
+      const float4 t = *reinterpret_cast<const float4*>(p.post_shift + co);
+      v.x = kpd_act(v.x * s.x + t.x, p.act2); v.y = kpd_act(v.y * s.y + t.y, p.act2);
+      v.z = kpd_act(v.z * s.z + t.z, p.act2); v.w = kpd_act(v.w * s.w + t.w, p.act2);
+    }
     if (p.res) {
       const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
       int sy = y, sx = x;
@@ -73,6 +86,10 @@ __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0
       if (p.rw != p.W) sx = min((int)floorf((float)x * ((float)p.rw / (float)p.W)), p.rw - 1);
       const float4 q = *reinterpret_cast<const float4*>(p.res + ((size_t)(n * p.rh + sy) * p.rw + sx) * p.cout_p + co);
       v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    }
+    if (p.act3) {
+      v.x = kpd_act(v.x, p.act3); v.y = kpd_act(v.y, p.act3);
+      v.z = kpd_act(v.z, p.act3); v.w = kpd_act(v.w, p.act3);
     }
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     store4<TO>(out + (size_t)m * p.out_cstride + co, v);

@@ -183,6 +183,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   e.bias = p.bias; e.out = p.out; e.res = p.res; e.stats = p.stats; e.amax = p.amax; e.scale = 1.f;
   e.M = M; e.H = H; e.W = W; e.cout_p = cout_p; e.out_cstride = p.out_cstride; e.rh = p.rh; e.rw = p.rw;
   e.act = p.act; e.tiles_per_img = p.tiles_per_img;
+  e.post_scale = p.post_scale; e.post_shift = p.post_shift; e.act2 = p.act2; e.act3 = p.act3;
   tile_store<TO, BM, BN>(tile, e, m0, n0);
 }
 
@@ -203,6 +204,7 @@ hipError_t launch_conv(const ConvArgs& a, ConvDType dt, int ks, hipStream_t st) 
     const bool bk32 = (a.cin_p % 32) == 0;
     if (ks == 3) {
       if (!bk32) return hipErrorInvalidValue;
+      if (a.cout_p <= 32) return launch<float, float, 3, 128, 32, 32>(a, st);
       if (a.cout_p <= 64) return launch<float, float, 3, 128, 64, 32>(a, st);
       return launch<float, float, 3, 128, 128, 32>(a, st);
     }

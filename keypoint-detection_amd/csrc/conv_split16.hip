@@ -159,6 +159,7 @@ __global__ __launch_bounds__(256) void conv3x3_split16_kernel(const Split16Args 
   ep.bias = p.bias; ep.out = p.out; ep.res = nullptr; ep.stats = p.stats; ep.amax = nullptr;
   ep.scale = out_scale; ep.M = M; ep.H = H; ep.W = W; ep.cout_p = cout_p; ep.out_cstride = cout_p;
   ep.rh = H; ep.rw = W; ep.act = p.act; ep.tiles_per_img = p.tiles_per_img;
+  ep.post_scale = nullptr; ep.post_shift = nullptr; ep.act2 = 0; ep.act3 = 0;
   tile_store<float, BM, BN>(tile, ep, m0, n0);
 }
 

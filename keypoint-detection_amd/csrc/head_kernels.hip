@@ -88,11 +88,15 @@ __global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, in
 // feat: FPN level-0 NHWC [B][Hf][Wf][Cf]; channel gather through topk (the
 // reference materialises features[b, topk] first -- here it is an index).
 // Also emits per-(roi,row) channel sum/max partials for HeatmapHead attention.
+// CW = channels per lane: 1 -> the 64 top-k channels (HeatmapHead input),
+// 2 -> all 128 FPN channels in order (KEYPOINT_HEAD input, topk == nullptr).
+template <int CW>
 __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
                                                         const int32_t* __restrict__ topk,
                                                         const float* __restrict__ boxes, int P,
                                                         float* __restrict__ roi, float* __restrict__ roi_stats) {
   __shared__ float red[4][2][TOPK];
+  constexpr int CO = TOPK * CW;
   const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* bx = boxes + (size_t)r * 4;
@@ -105,12 +109,16 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   const float bin_w = roi_w / (float)HM, bin_h = roi_h / (float)HM;
   const int gw = (int)ceilf(roi_w / (float)HM), gh = (int)ceilf(roi_h / (float)HM);
   const float count = (float)max(gw * gh, 1);
-  const int ch = topk[b * TOPK + lane];
-  const float* fb = feat + (size_t)b * Hf * Wf * Cf + ch;
+  const float* fb = feat + (size_t)b * Hf * Wf * Cf;
+  int ch[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) ch[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
 
   float s_sum = 0.f, s_max = -INFINITY;
   for (int pw = wave; pw < HM; pw += 4) {
-    float acc = 0.f;
+    float acc[CW];
+#pragma unroll
+    for (int q = 0; q < CW; ++q) acc[q] = 0.f;
     for (int iy = 0; iy < gh; ++iy) {
       float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
       for (int ix = 0; ix < gw; ++ix) {
@@ -121,16 +129,24 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
         if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
         if (xl >= Wf - 1) { xh = xl = Wf - 1; xx = (float)xl; } else xh = xl + 1;
         const float ly = yy - (float)yl, lx = xx - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
-        const float v1 = fb[((size_t)yl * Wf + xl) * Cf], v2 = fb[((size_t)yl * Wf + xh) * Cf];
-        const float v3 = fb[((size_t)yh * Wf + xl) * Cf], v4 = fb[((size_t)yh * Wf + xh) * Cf];
-        acc += hy * hx * v1 + hy * lx * v2 + ly * hx * v3 + ly * lx * v4;
+        const float* p1 = fb + ((size_t)yl * Wf + xl) * Cf;
+        const float* p2 = fb + ((size_t)yl * Wf + xh) * Cf;
+        const float* p3 = fb + ((size_t)yh * Wf + xl) * Cf;
+        const float* p4 = fb + ((size_t)yh * Wf + xh) * Cf;
+#pragma unroll
+        for (int q = 0; q < CW; ++q)
+          acc[q] += hy * hx * p1[ch[q]] + hy * lx * p2[ch[q]] + ly * hx * p3[ch[q]] + ly * lx * p4[ch[q]];
       }
     }
-    const float v = acc / count;
-    roi[(((size_t)r * HM + ph) * HM + pw) * TOPK + lane] = v;
-    s_sum += v;
-    s_max = fmaxf(s_max, v);
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const float v = acc[q] / count;
+      roi[(((size_t)r * HM + ph) * HM + pw) * CO + lane + TOPK * q] = v;
+      s_sum += v;
+      s_max = fmaxf(s_max, v);
+    }
   }
+  if (roi_stats == nullptr) return;   // (CW == 1 only) HeatmapHead attention partials
   red[wave][0][lane] = s_sum;
   red[wave][1][lane] = s_max;
   __syncthreads();
@@ -353,8 +369,14 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, float
 }
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk, const float* boxes,
                             int R, int P, float* roi, float* roi_stats, hipStream_t st) {
-  hipLaunchKernelGGL(roi_align_kernel, dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, topk, boxes, P, roi,
-                     roi_stats);
+  if (topk) {
+    hipLaunchKernelGGL((roi_align_kernel<1>), dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, topk, boxes, P, roi,
+                       roi_stats);
+  } else {
+    if (Cf != 2 * TOPK) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
+                       roi, nullptr);
+  }
   return hipGetLastError();
 }
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,

@@ -19,6 +19,9 @@ struct ConvArgs {
   int M;                 // N*H*W
   int tiles_per_img;
   float* amax;           // optional: atomicMax of |out| (float bits; caller zeroes it)
+  const float* post_scale;  // optional second affine after act (see conv_epilogue.h)
+  const float* post_shift;
+  int act2, act3;
 };
 
 // FPN level-0 3x3 conv on the f16 MFMA pipe with hi/lo operand split (conv_split16.hip)
@@ -70,4 +73,20 @@ hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_
 // ---- person head / NMS (nms.hip) ----
 hipError_t launch_nms(const float* boxes, const float* scores, int n, float thr, int max_out,
                       int32_t* keep, int32_t* n_keep, void* scratch, size_t scratch_bytes, hipStream_t st);
+// one workgroup per set; filter=1 starts candidates with score -inf dead; optional
+// zero-padded gather of the kept boxes/scores into out_boxes [sets][max_keep][4]
+hipError_t launch_nms_sets(const float* boxes, const float* scores, int sets, int n, float thr, int max_out,
+                           int max_keep, int32_t* keep, int32_t* n_keep, void* scratch, hipStream_t st, int filter,
+                           float* out_boxes, float* out_scores);
 size_t nms_scratch_bytes(int n);
+
+// ---- person-detector glue + KEYPOINT_HEAD (aux_heads.hip) ----
+hipError_t launch_adaptive_pool56(const float* in, int B, int Hf, int Wf, int C, float* out, hipStream_t st);
+hipError_t launch_person_decode(const float* head, int B, int hc, const float* anchors, int img_h, int img_w,
+                                float conf, float* cand_boxes, float* cand_scores, hipStream_t st);
+hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st);
+hipError_t launch_kh_pool(const float* in, int R, int C, int o, float* out, int out_stride, hipStream_t st);
+hipError_t launch_kh_final(const float* lin_r, int r_stride, const float* lin_v, int v_stride, const float* ln_rg,
+                           const float* ln_rb, const float* w_r, const float* b_r, const float* ln_vg,
+                           const float* ln_vb, const float* w_v, const float* b_v, const int32_t* slot, int R, int P,
+                           float* kh_kpts, float* kh_vis, hipStream_t st);

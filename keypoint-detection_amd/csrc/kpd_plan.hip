@@ -20,9 +20,6 @@
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 
-hipError_t launch_nms_sets(const float* boxes, const float* scores, int sets, int n, float thr, int max_out,
-                           int max_keep, int32_t* keep, int32_t* n_keep, void* scratch, hipStream_t st);
-
 namespace {
 
 thread_local std::string g_err;
@@ -111,15 +108,26 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* h3 = nullptr;
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
   float* amax = nullptr;  // max|lateral0| for the split16 FPN conv scale
+  // person-detector glue
+  float* pd_pool = nullptr;     // [B][56*56][128]
+  float* pd_head = nullptr;     // [B][56*56][48]
+  float* pd_boxes = nullptr;    // [B][28224][4]
+  float* pd_scores = nullptr;   // [B][28224]
+  int32_t* pd_keep = nullptr;   // [B][P]
+  int32_t* pd_nkeep = nullptr;  // [B]
+  uint8_t* pd_alive = nullptr;  // [B][28224]
+  // KEYPOINT_HEAD
+  float *kx = nullptr, *ksa = nullptr, *kds1 = nullptr, *krb1 = nullptr, *kds2 = nullptr, *krb2 = nullptr;
+  float *kr3 = nullptr, *kv1 = nullptr, *kpr = nullptr, *kpv = nullptr, *klr = nullptr, *klv = nullptr;
 };
 
 struct Dims {
-  int B = 0, H = 0, W = 0, NB = 0, P = 0;
+  int B = 0, H = 0, W = 0, NB = 0, P = 0, flags = 0;
   int h[12] = {}, w[12] = {};  // spatial dims after stem (0) and after bneck i (i+1)
   int Hf = 0, Wf = 0, tiles = 0;
   bool fused_stats = false;
   bool operator==(const Dims& o) const {
-    return B == o.B && H == o.H && W == o.W && NB == o.NB && P == o.P;
+    return B == o.B && H == o.H && W == o.W && NB == o.NB && P == o.P && flags == o.flags;
   }
 };
 
@@ -145,6 +153,18 @@ struct kpd_plan {
   struct { _Float16 *hi = nullptr, *lo = nullptr; int w_exp = 0; } fpn0s;  // split16 weights
   float *fin_w = nullptr, *fin_b = nullptr;
   float* zero_bias = nullptr;  // 128 zeros for bias-free laterals
+  // person-detector glue: box_heads[0] ++ cls_heads[0] as one 1x1 conv (45 -> 48 ch)
+  DevConv pd;
+  float* anchors = nullptr;    // [28224][4] reference buffer
+  float det_conf = 0.3f, det_iou = 0.3f;
+  // KEYPOINT_HEAD (present when keypoint_head.* tensors were registered)
+  bool has_kh = false;
+  int kh_o = 14;               // regression pool size (height // 4)
+  DevConv kh_sa1, kh_ds1, kh_rb1, kh_ds2, kh_rb2, kh_c3, kh_v1, kh_lr, kh_lv;
+  float *kh_sa2_w = nullptr, *kh_sa2_b = nullptr;
+  float *kh_bn1a_s = nullptr, *kh_bn1a_t = nullptr, *kh_bn1b_s = nullptr, *kh_bn1b_t = nullptr;
+  float *kh_lnr_g = nullptr, *kh_lnr_b = nullptr, *kh_fr_w = nullptr, *kh_fr_b = nullptr;
+  float *kh_lnv_g = nullptr, *kh_lnv_b = nullptr, *kh_fv_w = nullptr, *kh_fv_b = nullptr;
   // workspace
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -208,7 +228,8 @@ int pack_conv(kpd_plan* p, const std::string& wname, const std::string& bias_nam
     m = get(p, bn + ".running_mean", missing); v = get(p, bn + ".running_var", missing);
   }
   if (!w || (!bias_name.empty() && !cb) || (!bn.empty() && (!g || !b || !m || !v))) return KPD_ESTATE;
-  if (w->shape.size() != 4 || w->shape[2] != k || w->shape[3] != k)
+  const bool linear = w->shape.size() == 2 && k == 1;   // nn.Linear [out][in] as a 1x1 conv
+  if (!linear && (w->shape.size() != 4 || w->shape[2] != k || w->shape[3] != k))
     return fail(KPD_EINVAL, "bad shape for " + wname);
   dc.cout = (int)w->shape[0];
   dc.cin = (int)w->shape[1];
@@ -258,6 +279,22 @@ int pack_dw(kpd_plan* p, const std::string& pre, int k, int s, int act, DevDW& d
   }
   if (int rc = upload(p, pw, &dw.w)) return rc;
   return upload(p, pb, &dw.b);
+}
+
+// BatchNorm as a per-channel affine (scale, shift), padded to cout_p -- for a
+// BN that sits behind a non-linearity and cannot be folded into a conv.
+int pack_bn_affine(kpd_plan* p, const std::string& bn, int cout_p, float** s_out, float** t_out,
+                   std::string& missing) {
+  const HostT *g = get(p, bn + ".weight", missing), *b = get(p, bn + ".bias", missing);
+  const HostT *m = get(p, bn + ".running_mean", missing), *v = get(p, bn + ".running_var", missing);
+  if (!g || !b || !m || !v) return KPD_ESTATE;
+  const int n = (int)g->data.size();
+  std::vector<double> sc, sh;
+  bn_fold(g, b, m, v, 1e-5, n, nullptr, sc, sh);
+  std::vector<float> s(cout_p, 0.f), t(cout_p, 0.f);
+  for (int i = 0; i < n; ++i) { s[i] = (float)sc[i]; t[i] = (float)sh[i]; }
+  if (int rc = upload(p, s, s_out)) return rc;
+  return upload(p, t, t_out);
 }
 
 int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& missing, size_t expect = 0) {
@@ -337,8 +374,46 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
     w.h2 = c.take<char>(px * 256 * es);
     w.h3 = c.take<float>(px * 64);
     w.heat = c.take<float>(R * 17 * 3136);
+    if (d.flags & KPD_FLAG_DUAL_HEAD) {
+      const int o = p->kh_o;
+      w.kx = c.take<float>(px * 128);
+      w.ksa = c.take<float>(px * 64);
+      w.kds1 = c.take<float>(px * 64);
+      w.krb1 = c.take<float>(px * 64);
+      w.kds2 = c.take<float>(px * 32);
+      w.krb2 = c.take<float>(px * 32);
+      w.kr3 = c.take<float>(px * 16);
+      w.kv1 = c.take<float>(px * 32);
+      w.kpr = c.take<float>(R * (size_t)pad16(16 * o * o));
+      w.kpv = c.take<float>(R * 512);
+      w.klr = c.take<float>(R * 256);
+      w.klv = c.take<float>(R * 128);
+    }
+  }
+  if (d.flags & KPD_FLAG_DETECT) {
+    const size_t na = (size_t)B * 3136 * 9;
+    w.pd_pool = c.take<float>((size_t)B * 3136 * 128);
+    w.pd_head = c.take<float>((size_t)B * 3136 * 48);
+    w.pd_boxes = c.take<float>(na * 4);
+    w.pd_scores = c.take<float>(na);
+    w.pd_keep = c.take<int32_t>((size_t)B * std::max(d.P, 1));
+    w.pd_nkeep = c.take<int32_t>(B);
+    w.pd_alive = c.take<uint8_t>(na);
   }
   return c.off + 256;
+}
+
+// conv with the second affine + residual + final activation epilogue
+int conv_post(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, void* out, int act,
+              const float* ps, const float* pt, int act2, const float* res, int act3, hipStream_t st) {
+  ConvArgs a{};
+  a.in = in; a.wt = L.w; a.bias = L.b; a.out = out; a.res = res;
+  a.N = N; a.H = H; a.W = W; a.cin_p = L.cin_p; a.cout_p = L.cout_p;
+  a.in_cstride = in_cstride; a.out_cstride = L.cout_p;
+  a.rh = H; a.rw = W; a.act = act; a.M = N * H * W;
+  a.post_scale = ps; a.post_shift = pt; a.act2 = act2; a.act3 = act3;
+  HIP_TRY(launch_conv(a, CONV_F32, L.k, st));
+  return KPD_OK;
 }
 
 // RAII stage marker: records a start/end event pair on the launch stream
@@ -431,6 +506,11 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   for (void* a : p->allocs) (void)hipFree(a);
   p->allocs.clear();
   p->fpn0s.hi = p->fpn0s.lo = nullptr;
+  p->pd = DevConv();
+  p->anchors = nullptr;
+  p->kh_ds1 = DevConv();
+  p->kh_ds2 = DevConv();
+  p->has_kh = false;
   if (p->ws) { (void)hipFree(p->ws); p->ws = nullptr; p->ws_bytes = 0; }
   p->have_work = false;
   p->precision = precision;
@@ -515,6 +595,71 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     std::vector<float> z(128, 0.f);
     chk(upload(p, z, &p->zero_bias));
   }
+  // person-detector glue: box_heads[0] ++ cls_heads[0] -> one 1x1 conv (45 outputs)
+  {
+    const HostT* bw = get(p, "person_detector.box_heads.0.weight", missing);
+    const HostT* bb = get(p, "person_detector.box_heads.0.bias", missing);
+    const HostT* cw = get(p, "person_detector.cls_heads.0.weight", missing);
+    const HostT* cb = get(p, "person_detector.cls_heads.0.bias", missing);
+    const HostT* an = get(p, "person_detector.anchors", missing);
+    if (bw && bb && cw && cb && an) {
+      if (bw->shape[0] != 36 || cw->shape[0] != 9 || an->data.size() != (size_t)56 * 56 * 9 * 4)
+        return fail(KPD_EINVAL, "person head expects 9 anchors on the 56x56 grid (1 class)");
+      HostT w, b;
+      w.shape = {45, bw->shape[1], 1, 1};
+      w.data = bw->data;
+      w.data.insert(w.data.end(), cw->data.begin(), cw->data.end());
+      b.shape = {45};
+      b.data = bb->data;
+      b.data.insert(b.data.end(), cb->data.begin(), cb->data.end());
+      p->t["__pd.weight"] = std::move(w);
+      p->t["__pd.bias"] = std::move(b);
+      chk(pack_conv(p, "__pd.weight", "__pd.bias", "", 0, 1, false, p->pd, missing));
+      chk(upload(p, an->data, &p->anchors));
+    }
+  }
+  // KEYPOINT_HEAD (optional)
+  p->has_kh = p->t.count("keypoint_head.spatial_attention.0.weight") > 0;
+  if (p->has_kh) {
+    const std::string K = "keypoint_head.", R = K + "regression_branch.", V = K + "visibility_branch.";
+    chk(pack_conv(p, K + "spatial_attention.0.weight", K + "spatial_attention.0.bias", "", 0, 1, false, p->kh_sa1,
+                  missing));
+    chk(pack_plain(p, K + "spatial_attention.2.weight", &p->kh_sa2_w, missing, 64));
+    chk(pack_plain(p, K + "spatial_attention.2.bias", &p->kh_sa2_b, missing, 1));
+    DevConv* ds[2] = {&p->kh_ds1, &p->kh_ds2};
+    DevConv* rb[2] = {&p->kh_rb1, &p->kh_rb2};
+    float** bs[2] = {&p->kh_bn1a_s, &p->kh_bn1b_s};
+    float** bt[2] = {&p->kh_bn1a_t, &p->kh_bn1b_t};
+    for (int i = 0; i < 2; ++i) {
+      const std::string B = R + std::to_string(i) + ".";
+      chk(pack_conv(p, B + "conv1.0.weight", B + "conv1.0.bias", B + "conv1.1", 1e-5, 3, false, *rb[i], missing));
+      if (p->t.count(B + "downsample.0.weight"))
+        chk(pack_conv(p, B + "downsample.0.weight", B + "downsample.0.bias", B + "downsample.1", 1e-5, 1, false,
+                      *ds[i], missing));
+      chk(pack_bn_affine(p, B + "bn1", rb[i]->cout_p ? rb[i]->cout_p : 64, bs[i], bt[i], missing));
+    }
+    chk(pack_conv(p, R + "2.weight", R + "2.bias", R + "3", 1e-5, 3, false, p->kh_c3, missing));
+    chk(pack_conv(p, R + "7.weight", R + "7.bias", "", 0, 1, false, p->kh_lr, missing));
+    chk(pack_plain(p, R + "8.weight", &p->kh_lnr_g, missing, 256));
+    chk(pack_plain(p, R + "8.bias", &p->kh_lnr_b, missing, 256));
+    chk(pack_plain(p, R + "11.weight", &p->kh_fr_w, missing, 34 * 256));
+    chk(pack_plain(p, R + "11.bias", &p->kh_fr_b, missing, 34));
+    chk(pack_conv(p, V + "0.weight", V + "0.bias", V + "1", 1e-5, 3, false, p->kh_v1, missing));
+    chk(pack_conv(p, V + "5.weight", V + "5.bias", "", 0, 1, false, p->kh_lv, missing));
+    chk(pack_plain(p, V + "6.weight", &p->kh_lnv_g, missing, 128));
+    chk(pack_plain(p, V + "6.bias", &p->kh_lnv_b, missing, 128));
+    chk(pack_plain(p, V + "9.weight", &p->kh_fv_w, missing, 51 * 128));
+    chk(pack_plain(p, V + "9.bias", &p->kh_fv_b, missing, 51));
+    if (rc == KPD_OK && missing.empty()) {
+      const int in = p->kh_lr.cin;
+      int o = 1;
+      while (16 * (o + 1) * (o + 1) <= in) ++o;
+      if (16 * o * o != in || p->kh_c3.cout != 16 || p->kh_v1.cout != 32 || p->kh_lv.cin != 512 ||
+          p->kh_sa1.cin != 128 || p->kh_sa1.cout != 64)
+        return fail(KPD_EINVAL, "KEYPOINT_HEAD shape not supported (needs in 128, regression 32, square pool)");
+      p->kh_o = o;
+    }
+  }
   if (!missing.empty()) return fail(KPD_ESTATE, "missing tensors: " + missing);
   if (rc != KPD_OK) return rc;
   // shape checks the kernels rely on
@@ -542,19 +687,26 @@ static int ensure_work(kpd_plan* p, const Dims& d) {
   return KPD_OK;
 }
 
-int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, const float* boxes, int NB, int P,
-                float* kpts, float* vis, float* heat, int32_t* topk_out, void* stream) {
+int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
+                int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis, float* box_scores,
+                int32_t* topk_out, void* stream) {
   if (!p) return fail(KPD_EINVAL, "null plan");
   if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
   if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
   if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
+  if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD)) return fail(KPD_EINVAL, "unknown flags");
+  const bool detect = flags & KPD_FLAG_DETECT, dual = flags & KPD_FLAG_DUAL_HEAD;
+  if (detect && (NB != B || P <= 0 || !boxes)) return fail(KPD_EINVAL, "detect mode: boxes must be [B][P>0][4]");
+  if (detect && !p->anchors) return fail(KPD_ESTATE, "person detector weights missing");
+  if (dual && !p->has_kh) return fail(KPD_ESTATE, "dual head requested but no keypoint_head.* weights");
+  if (dual && NB * P > 0 && (!kh_kpts || !kh_vis)) return fail(KPD_EINVAL, "null dual-head output pointer");
   if (NB < 0 || NB > B || P < 0) return fail(KPD_EINVAL, "bad box batch");
   if (NB * P > 0 && (!boxes || !kpts || !vis)) return fail(KPD_EINVAL, "null box/output pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipSetDevice(p->device));
 
   Dims d;
-  d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P;
+  d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P; d.flags = flags;
   d.h[0] = (H - 1) / 2 + 1; d.w[0] = (W - 1) / 2 + 1;
   for (int i = 0; i < 11; ++i) {
     const int k = kBneck[i].k, s = kBneck[i].s, pd = (k - 1) / 2;
@@ -641,6 +793,19 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, con
   p->debug["tap2"] = {taps[2], sizeof(float) * (size_t)B * lh[2] * lw[2] * pad16(48)};
   p->debug["tap3"] = {taps[3], sizeof(float) * (size_t)B * lh[3] * lw[3] * 576};
 
+  // ---------------- person-detector glue (boxes become an output) ----------------
+  if (detect) {
+    Stage sg(p, "person_detect", st);
+    HIP_TRY(launch_adaptive_pool56(w.feat, B, d.Hf, d.Wf, 128, w.pd_pool, st));
+    if (int rc = conv(p->pd, w.pd_pool, B, 56, 56, 128, w.pd_head, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0,
+                      st))
+      return rc;
+    HIP_TRY(launch_person_decode(w.pd_head, B, p->pd.cout_p, p->anchors, H, W, p->det_conf, w.pd_boxes,
+                                 w.pd_scores, st));
+    HIP_TRY(launch_nms_sets(w.pd_boxes, w.pd_scores, B, 56 * 56 * 9, p->det_iou, P, P, w.pd_keep, w.pd_nkeep,
+                            w.pd_alive, st, 1, boxes, box_scores));
+  }
+
   const int R = NB * P;
   if (R == 0) return KPD_OK;
 
@@ -681,6 +846,63 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, con
     HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
     HIP_TRY(launch_decode(heat_out, boxes, w.slot, R, P, kpts, vis, st));
   }
+  if (dual) {
+    // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
+    Stage sg(p, "keypoint_head", st);
+    const size_t px = (size_t)R * 3136;
+    HIP_TRY(hipMemsetAsync(kh_kpts, 0, nkp * 2 * sizeof(float), st));
+    HIP_TRY(hipMemsetAsync(kh_vis, 0, nkp * 3 * sizeof(float), st));
+    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
+    if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    HIP_TRY(launch_kh_att(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, px, st));
+    // ResidualBlock(128 -> 64): relu6(relu6(bn1(relu6(conv_bn(x)))) + downsample(x))
+    const float* id1 = w.kx;
+    if (p->kh_ds1.w) {
+      if (int rc = conv(p->kh_ds1, w.kx, R, 56, 56, 128, w.kds1, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+        return rc;
+      id1 = w.kds1;
+    }
+    if (int rc = conv_post(p->kh_rb1, w.kx, R, 56, 56, 128, w.krb1, ACT_RELU6, p->kh_bn1a_s, p->kh_bn1a_t,
+                           ACT_RELU6, id1, ACT_RELU6, st))
+      return rc;
+    const float* id2 = w.krb1;
+    if (p->kh_ds2.w) {
+      if (int rc = conv(p->kh_ds2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.kds2, ACT_NONE, nullptr, 0, 0, nullptr,
+                        nullptr, 0, 0, st))
+        return rc;
+      id2 = w.kds2;
+    }
+    if (int rc = conv_post(p->kh_rb2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.krb2, ACT_RELU6, p->kh_bn1b_s,
+                           p->kh_bn1b_t, ACT_RELU6, id2, ACT_RELU6, st))
+      return rc;
+    if (int rc = conv(p->kh_c3, w.krb2, R, 56, 56, p->kh_rb2.cout_p, w.kr3, ACT_RELU6, nullptr, 0, 0, nullptr,
+                      nullptr, 0, 0, st))
+      return rc;
+    if (int rc = conv(p->kh_v1, w.kx, R, 56, 56, 128, w.kv1, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    const int o = p->kh_o, kr = pad16(16 * o * o);
+    if (kr != 16 * o * o) HIP_TRY(hipMemsetAsync(w.kpr, 0, sizeof(float) * R * kr, st));
+    HIP_TRY(launch_kh_pool(w.kr3, R, 16, o, w.kpr, kr, st));
+    HIP_TRY(launch_kh_pool(w.kv1, R, 32, 4, w.kpv, 512, st));
+    // the two Linear layers as 1x1 MFMA GEMMs over all ROIs (M = R)
+    if (int rc = conv(p->kh_lr, w.kpr, R, 1, 1, kr, w.klr, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    if (int rc = conv(p->kh_lv, w.kpv, R, 1, 1, 512, w.klv, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    HIP_TRY(launch_kh_final(w.klr, p->kh_lr.cout_p, w.klv, p->kh_lv.cout_p, p->kh_lnr_g, p->kh_lnr_b, p->kh_fr_w,
+                            p->kh_fr_b, p->kh_lnv_g, p->kh_lnv_b, p->kh_fv_w, p->kh_fv_b, w.slot, R, P, kh_kpts,
+                            kh_vis, st));
+  }
+  return KPD_OK;
+}
+
+int kpd_plan_set_detector(kpd_plan* p, float conf_threshold, float nms_iou_threshold) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  if (!(conf_threshold >= 0.f && conf_threshold <= 1.f) || !(nms_iou_threshold >= 0.f && nms_iou_threshold <= 1.f))
+    return fail(KPD_EINVAL, "thresholds must be in [0, 1]");
+  p->det_conf = conf_threshold;
+  p->det_iou = nms_iou_threshold;
   return KPD_OK;
 }
 
@@ -727,7 +949,8 @@ int kpd_nms(const float* boxes, const float* scores, int n, float thr, int max_o
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   void* scratch = nullptr;
   if (n > 0) HIP_TRY(hipMallocAsync(&scratch, (size_t)n, st));
-  const hipError_t e = launch_nms_sets(boxes, scores, 1, n, thr, max_out, std::max(n, 1), keep, n_keep, scratch, st);
+  const hipError_t e =
+      launch_nms_sets(boxes, scores, 1, n, thr, max_out, std::max(n, 1), keep, n_keep, scratch, st, 0, nullptr, nullptr);
   if (scratch) HIP_TRY(hipFreeAsync(scratch, st));
   HIP_TRY(e);
   return KPD_OK;

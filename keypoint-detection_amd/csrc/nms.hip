@@ -43,7 +43,8 @@ __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
 __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                                                    int n, float thr, int max_out, int max_keep,
                                                    int32_t* __restrict__ keep, int32_t* __restrict__ n_keep,
-                                                   uint8_t* __restrict__ alive_all) {
+                                                   uint8_t* __restrict__ alive_all, int filter,
+                                                   float* __restrict__ out_boxes, float* __restrict__ out_scores) {
   __shared__ float ws[16];
   __shared__ int wi[16];
   __shared__ int best_s;
@@ -51,7 +52,8 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
   const float* bx = boxes + (size_t)set * n * 4;
   const float* sc = scores + (size_t)set * n;
   uint8_t* alive = alive_all + (size_t)set * n;
-  for (int i = tid; i < n; i += 1024) alive[i] = 1;
+  // filter: candidates whose score is -inf (below the detector's conf threshold) start dead
+  for (int i = tid; i < n; i += 1024) alive[i] = filter ? (sc[i] > -INFINITY) : 1;
   __syncthreads();
   int kept = 0;
   const int limit = max_out > 0 ? min(max_out, max_keep) : max_keep;
@@ -90,6 +92,20 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
     __syncthreads();
   }
   if (tid == 0) n_keep[set] = kept;
+  if (out_boxes) {   // gather kept boxes, zero padded to max_keep (zero boxes are skipped downstream)
+    __syncthreads();
+    for (int t = tid; t < max_keep; t += 1024) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float s = 0.f;
+      if (t < kept) {
+        const int k = keep[(size_t)set * max_keep + t];
+        v = *reinterpret_cast<const float4*>(bx + (size_t)k * 4);
+        s = sc[k];
+      }
+      *reinterpret_cast<float4*>(out_boxes + ((size_t)set * max_keep + t) * 4) = v;
+      if (out_scores) out_scores[(size_t)set * max_keep + t] = s;
+    }
+  }
 }
 
 }  // namespace
@@ -97,17 +113,18 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
 size_t nms_scratch_bytes(int n) { return (size_t)n; }
 
 hipError_t launch_nms_sets(const float* boxes, const float* scores, int sets, int n, float thr, int max_out,
-                           int max_keep, int32_t* keep, int32_t* n_keep, void* scratch, hipStream_t st) {
+                           int max_keep, int32_t* keep, int32_t* n_keep, void* scratch, hipStream_t st, int filter,
+                           float* out_boxes, float* out_scores) {
   if (n <= 0) {
     return hipMemsetAsync(n_keep, 0, sizeof(int32_t) * sets, st);
   }
   hipLaunchKernelGGL(nms_kernel, dim3(sets), dim3(1024), 0, st, boxes, scores, n, thr, max_out, max_keep, keep,
-                     n_keep, reinterpret_cast<uint8_t*>(scratch));
+                     n_keep, reinterpret_cast<uint8_t*>(scratch), filter, out_boxes, out_scores);
   return hipGetLastError();
 }
 
 hipError_t launch_nms(const float* boxes, const float* scores, int n, float thr, int max_out, int32_t* keep,
                       int32_t* n_keep, void* scratch, size_t scratch_bytes, hipStream_t st) {
   if (scratch_bytes < nms_scratch_bytes(n)) return hipErrorInvalidValue;
-  return launch_nms_sets(boxes, scores, 1, n, thr, max_out, n, keep, n_keep, scratch, st);
+  return launch_nms_sets(boxes, scores, 1, n, thr, max_out, n, keep, n_keep, scratch, st, 0, nullptr, nullptr);
 }

@@ -22,9 +22,11 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "mixed": KPD_PRECISION_MIXED, "bf16": 
 # every symbol include/kpd.h declares (checked by tests/test_abi.py)
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
-           "kpd_plan_timing", "kpd_plan_timing_query")
-STAGES = ("body", "fpn_lateral", "fpn0", "topk", "roi_align", "hm_attention", "hm_conv1", "hm_conv2",
-          "hm_conv3", "hm_final_decode")
+           "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector")
+FLAG_DETECT = 1
+FLAG_DUAL_HEAD = 2
+STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",
+          "hm_conv2", "hm_conv3", "hm_final_decode", "keypoint_head")
 
 
 class KpdNativeError(RuntimeError):
@@ -52,8 +54,9 @@ def load() -> ctypes.CDLL:
     lib.kpd_plan_finalize.argtypes = [c_void_p, c_int]
     lib.kpd_plan_destroy.argtypes = [c_void_p]
     lib.kpd_plan_destroy.restype = None
-    lib.kpd_forward.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
-                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kpd_forward.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kpd_plan_set_detector.argtypes = [c_void_p, ctypes.c_float, ctypes.c_float]
     lib.kpd_debug_copy.argtypes = [c_void_p, c_char_p, c_void_p, ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), c_void_p]
     lib.kpd_plan_timing.argtypes = [c_void_p, c_int]
@@ -114,13 +117,20 @@ class Plan:
     def finalize(self, precision: int) -> None:
         check(self.lib.kpd_plan_finalize(self.h, precision), "kpd_plan_finalize")
 
-    def forward(self, image: torch.Tensor, boxes: Optional[torch.Tensor], kpts, vis, heat, topk=None) -> None:
+    def set_detector(self, conf_threshold: float, nms_iou_threshold: float) -> None:
+        check(self.lib.kpd_plan_set_detector(self.h, float(conf_threshold), float(nms_iou_threshold)),
+              "kpd_plan_set_detector")
+
+    def forward(self, image: torch.Tensor, boxes: Optional[torch.Tensor], kpts, vis, heat, flags: int = 0,
+                kh_kpts=None, kh_vis=None, box_scores=None, topk=None) -> None:
+        """boxes [nb,P,4] (input; an output filled by the detector with FLAG_DETECT)."""
         _require_cuda(image, "image")
         B, C, H, W = image.shape
         nb, P = (0, 0) if boxes is None else (boxes.shape[0], boxes.shape[1])
         with torch.cuda.device(self.device):
-            check(self.lib.kpd_forward(self.h, _ptr(image), B, C, H, W, _ptr(boxes), nb, P, _ptr(kpts), _ptr(vis),
-                                       _ptr(heat), _ptr(topk), _stream(self.device)), "kpd_forward")
+            check(self.lib.kpd_forward(self.h, _ptr(image), B, C, H, W, _ptr(boxes), nb, P, int(flags), _ptr(kpts),
+                                       _ptr(vis), _ptr(heat), _ptr(kh_kpts), _ptr(kh_vis), _ptr(box_scores),
+                                       _ptr(topk), _stream(self.device)), "kpd_forward")
 
     def timing(self, enable: bool) -> None:
         check(self.lib.kpd_plan_timing(self.h, 1 if enable else 0), "kpd_plan_timing")

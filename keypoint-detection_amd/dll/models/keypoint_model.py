@@ -78,7 +78,7 @@ class MultiPersonKeypointModel(nn.Module):
     """
 
     def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "fp32",
-                 dual_head: bool = False):
+                 dual_head: bool = False, max_persons: int = 5):
         super().__init__()
         if precision not in _native.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_native.PRECISIONS)}")
@@ -88,8 +88,10 @@ class MultiPersonKeypointModel(nn.Module):
         self.person_detector = PERSON_HEAD(config.person_head)
         self.heatmap_head = HeatmapHead(config.heatmap_head)
         self.channel_attention = ChannelAttention(config.backbone.out_channels, reduction_ratio=16)
+        self.dual_head = dual_head
         if dual_head:
             self.keypoint_head = KEYPOINT_HEAD(config.keypoint_head)
+        self.max_persons = max_persons
         self.num_keypoints = config.num_keypoints
         self.precision = precision
         self._plan: Optional[_native.Plan] = None
@@ -112,6 +114,8 @@ class MultiPersonKeypointModel(nn.Module):
                 if t.is_floating_point():
                     plan.set_tensor(name, t)
             plan.finalize(_native.PRECISIONS[self.precision])
+            ph = self.config.person_head
+            plan.set_detector(ph.conf_threshold, ph.nms_iou_threshold)
             self._plan, self._plan_key = plan, key
         return self._plan
 
@@ -133,10 +137,20 @@ class MultiPersonKeypointModel(nn.Module):
         K = self.num_keypoints
         dev = x.device
         boxes = normalize_bboxes(batch, B, dev)
-        if boxes is None:
-            raise NotImplementedError("person-detector branch (no 'bboxes') is not wired yet; pass boxes")
         plan = self.native_plan(dev)
         image = x.float().contiguous()
+        flags = _native.FLAG_DUAL_HEAD if self.dual_head else 0
+        if boxes is None:
+            # person-detector branch (reference :114-119 is broken; build-defined
+            # glue: FPN0 -> 56x56 pool -> box/cls heads -> decode -> NMS,
+            # DESIGN.md §C3).  Detected boxes are zero padded to max_persons.
+            P = self.max_persons
+            bt = torch.zeros(B, P, 4, device=dev)
+            scores = torch.zeros(B, P, device=dev)
+            out = self._run(plan, image, bt, B, P, flags | _native.FLAG_DETECT, scores)
+            out["boxes"] = [bt[i] for i in range(B)]
+            out["box_scores"] = scores
+            return out
         if not boxes or all(len(b) == 0 for b in boxes):
             return {"keypoints": torch.zeros(B, 1, K, 2, device=dev),
                     "visibilities": torch.zeros(B, 1, K, device=dev),
@@ -149,8 +163,21 @@ class MultiPersonKeypointModel(nn.Module):
         bt = torch.stack([b.to(dev, torch.float32) for b in boxes]).contiguous()   # [nb,P,4]
         if bt.dim() != 3 or bt.size(-1) != 4:
             raise ValueError(f"Invalid bboxes format: {tuple(bt.shape)}")
+        out = self._run(plan, image, bt, nb, P, flags)
+        out["boxes"] = boxes
+        return out
+
+    def _run(self, plan, image, bt, nb, P, flags, box_scores=None) -> Dict[str, torch.Tensor]:
+        dev, K = image.device, self.num_keypoints
         kpts = torch.empty(nb, P, 1, K, 2, device=dev)
         vis = torch.empty(nb, P, 1, K, 3, device=dev)
         heat = torch.empty(nb, P, K, HEATMAP_SIDE, HEATMAP_SIDE, device=dev)
-        plan.forward(image, bt, kpts, vis, heat)
-        return {"heatmap": heat, "keypoints": kpts, "visibilities": vis, "boxes": boxes}
+        kh_k = kh_v = None
+        if flags & _native.FLAG_DUAL_HEAD:
+            kh_k = torch.empty(nb, P, 1, K, 2, device=dev)
+            kh_v = torch.empty(nb, P, 1, K, 3, device=dev)
+        plan.forward(image, bt, kpts, vis, heat, flags, kh_k, kh_v, box_scores)
+        out = {"heatmap": heat, "keypoints": kpts, "visibilities": vis}
+        if kh_k is not None:
+            out["kh_keypoints"], out["kh_visibilities"] = kh_k, kh_v
+        return out

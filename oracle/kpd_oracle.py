@@ -353,7 +353,12 @@ def normalize_bboxes(batch, batch_size: int) -> Optional[List[Tensor]]:
 # full eval forward with caller-given boxes (keypoint_model.py:73-210)
 # --------------------------------------------------------------------------
 @torch.no_grad()
-def forward(sd: SD, batch, return_debug: bool = False):
+def forward(sd: SD, batch, return_debug: bool = False, dual_head: bool = False, kh_size: int = 56,
+            detect: Optional[dict] = None):
+    """Eval forward.  ``detect`` (dict of person_detect kwargs) enables the
+    build-defined detector glue when the batch carries no 'bboxes';
+    ``dual_head`` also runs KEYPOINT_HEAD ("keypoint_head." weights) on the
+    128-channel ROI features (outputs 'kh_keypoints' / 'kh_visibilities')."""
     x = batch["image"] if isinstance(batch, dict) else batch
     if not isinstance(x, torch.Tensor):
         raise TypeError("Input must be a tensor or a dict with 'image' key containing a tensor")
@@ -363,7 +368,10 @@ def forward(sd: SD, batch, return_debug: bool = False):
     feats, topk = select_top_k(feat0, sd)
     boxes = normalize_bboxes(batch, B)
     if boxes is None:
-        raise NotImplementedError("person-detector branch: see person_detector_forward")
+        if detect is None:
+            raise NotImplementedError("person-detector branch: pass detect=dict(...)")
+        det, _ = person_detect(feat0, sd, x.shape[2], x.shape[3], **detect)
+        boxes = [det[b] for b in range(B)]
     K = NUM_KEYPOINTS
     if not boxes or all(len(b) == 0 for b in boxes):
         out = {"keypoints": torch.zeros(B, 1, K, 2), "visibilities": torch.zeros(B, 1, K),
@@ -372,9 +380,9 @@ def forward(sd: SD, batch, return_debug: bool = False):
             out["_feat0"] = feat0; out["_topk"] = topk
         return out
     pmax = max(len(b) for b in boxes)
-    ph, pk, pv = [], [], []
+    ph, pk, pv, pkk, pkv = [], [], [], [], []
     for bi, bx in enumerate(boxes):
-        hs, ks, vs = [], [], []
+        hs, ks, vs, kks, kvs = [], [], [], [], []
         for box in bx:
             box = box.float()
             if torch.all(box == 0) or box.shape[-1] != 4:
@@ -384,13 +392,23 @@ def forward(sd: SD, batch, return_debug: bool = False):
             kp, vis = decode_heatmap(hm)
             kp = to_image_coords(kp, box)
             hs.append(hm); ks.append(kp); vs.append(vis)
+            if dual_head:
+                r128 = extract_roi_features(feat0[bi:bi + 1], box)
+                a, v = keypoint_head(r128, sd, "keypoint_head.", K, kh_size, kh_size)
+                kks.append(a); kvs.append(v)
         if not ks:
             dv = torch.zeros(1, K, 3); dv[:, :, 0] = 1.0
             ks.append(torch.zeros(1, K, 2)); hs.append(torch.zeros(1, K, 56, 56)); vs.append(dv)
+            kks.append(torch.zeros(1, K, 2)); kvs.append(torch.zeros(1, K, 3))
         ks, hs, vs = pad_to_length(ks, pmax), pad_to_length(hs, pmax), pad_to_length(vs, pmax)
         pk.append(torch.stack(ks)); ph.append(torch.stack(hs)); pv.append(torch.stack(vs))
+        if dual_head:
+            pkk.append(torch.stack(pad_to_length(kks, pmax))); pkv.append(torch.stack(pad_to_length(kvs, pmax)))
     out = {"heatmap": torch.stack(ph).squeeze(2), "keypoints": torch.stack(pk),
            "visibilities": torch.stack(pv), "boxes": boxes}
+    if dual_head:
+        out["kh_keypoints"] = torch.stack(pkk)
+        out["kh_visibilities"] = torch.stack(pkv)
     if return_debug:
         out["_feat0"] = feat0; out["_topk"] = topk
     return out
@@ -444,6 +462,50 @@ def nms(boxes: Tensor, scores: Tensor, iou_threshold: float = 0.2,
         iou = box_iou_cxcywh(boxes[i].unsqueeze(0), boxes[order])
         order = order[(iou <= iou_threshold).squeeze(0)]
     return torch.tensor(keep, dtype=torch.int64)
+
+
+# --------------------------------------------------------------------------
+# Person-detector glue (build-defined; the reference's PERSON_HEAD.forward
+# never decodes boxes nor runs NMS, person_head.py:141-166 -- DESIGN.md §C3):
+#   1. FPN level 0 (128 ch) adaptive-avg-pooled to the anchor grid 56x56
+#   2. box_heads[0] / cls_heads[0] 1x1 convs (36 = 9 anchors x 4, 9 logits)
+#   3. score = sigmoid(logit); candidates score > conf_threshold
+#   4. decode against the reference's anchors buffer, anchor w/h in pixels
+#      normalised by the input width/height:
+#        cx = ax + dx*aw, cy = ay + dy*ah, w = aw*exp(min(dw, 4.135)), h = ...
+#   5. greedy NMS (person_head.py:96-139), keep <= max_persons, zero padded
+# --------------------------------------------------------------------------
+BBOX_CLIP = math.log(1000.0 / 16)
+
+
+def person_detect(feat0: Tensor, sd: SD, img_h: int, img_w: int, conf_threshold: float = 0.3,
+                  iou_threshold: float = 0.3, max_persons: int = 5,
+                  p: str = "person_detector.") -> Tuple[Tensor, Tensor]:
+    B = feat0.shape[0]
+    g = F.adaptive_avg_pool2d(feat0, (56, 56))
+    box = F.conv2d(g, sd[p + "box_heads.0.weight"], sd[p + "box_heads.0.bias"])     # [B,36,56,56]
+    cls = F.conv2d(g, sd[p + "cls_heads.0.weight"], sd[p + "cls_heads.0.bias"])     # [B,9,56,56]
+    box = box.permute(0, 2, 3, 1).reshape(B, -1, 4)                                  # [(i,j,a)] order
+    score = torch.sigmoid(cls.permute(0, 2, 3, 1).reshape(B, -1))
+    anc = sd[p + "anchors"]
+    aw = anc[:, 2] / img_w
+    ah = anc[:, 3] / img_h
+    cx = anc[:, 0] + box[..., 0] * aw
+    cy = anc[:, 1] + box[..., 1] * ah
+    w = aw * torch.exp(torch.clamp(box[..., 2], max=BBOX_CLIP))
+    h = ah * torch.exp(torch.clamp(box[..., 3], max=BBOX_CLIP))
+    dec = torch.stack([cx, cy, w, h], dim=-1)
+    out = torch.zeros(B, max_persons, 4)
+    out_s = torch.zeros(B, max_persons)
+    for b in range(B):
+        cand = torch.nonzero(score[b] > conf_threshold).flatten()
+        if cand.numel() == 0:
+            continue
+        keep = nms(dec[b, cand], score[b, cand], iou_threshold, max_persons)
+        k = cand[keep]
+        out[b, :len(k)] = dec[b, k]
+        out_s[b, :len(k)] = score[b, k]
+    return out, out_s
 
 
 # --------------------------------------------------------------------------

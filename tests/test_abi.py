@@ -36,8 +36,9 @@ def test_plan_argument_validation():
     assert b"in_channels" in lib.kpd_last_error()
     assert lib.kpd_plan_create(0, 3, ctypes.byref(h)) == 0
     # forward before finalize -> KPD_ESTATE
-    rc = lib.kpd_forward(h, None, 1, 3, 64, 64, None, 0, 0, None, None, None, None, None)
+    rc = lib.kpd_forward(h, None, 1, 3, 64, 64, None, 0, 0, 0, None, None, None, None, None, None, None, None)
     assert rc == -3 and b"finalized" in lib.kpd_last_error()
+    assert lib.kpd_plan_set_detector(h, 1.5, 0.3) == -1
     # finalize without weights -> missing tensors listed (or no HIP device here)
     rc = lib.kpd_plan_finalize(h, 0)
     assert rc in (-2, -3)

@@ -192,6 +192,54 @@ def test_nms_gpu_vs_golden(golden_dir):
         i += 1
 
 
+def _dual_model(precision="fp32"):
+    from dll.configs import KeypointHeadConfig, ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_state_dict
+    m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
+                                 TrainingConfig(), precision=precision, dual_head=True)
+    sd = synthetic_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    return m.to(DEV).eval(), sd
+
+
+def test_dual_head_vs_oracle():
+    """KEYPOINT_HEAD on 128-channel ROI features (§8 a11): native vs the oracle
+    restatement (itself pinned to the reference module's goldens)."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m, sd = _dual_model()
+    img = synthetic_images(2, 3, 256, 192, seed=41)
+    boxes = synthetic_boxes(2, 3, seed=42)
+    boxes[1, 0] = 0.0
+    with torch.no_grad():
+        out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    ref = O.forward(sd, {"image": img, "bboxes": boxes}, dual_head=True)
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    np.testing.assert_allclose(out["kh_keypoints"].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=1e-5)
+    np.testing.assert_allclose(out["kh_visibilities"].cpu().numpy(), ref["kh_visibilities"].numpy(), atol=1e-5)
+
+
+def test_person_detector_glue_vs_oracle():
+    """No 'bboxes' -> build-defined detector glue (§8 a10): pooled 1x1 heads,
+    anchor decode, threshold, NMS (max 5).  Checked against the oracle on the
+    same FPN features, then the keypoint stage on the detected boxes."""
+    from dll.models.synthetic import synthetic_images
+    m, sd = _dual_model()
+    img = synthetic_images(3, 3, 256, 192, seed=51)
+    with torch.no_grad():
+        out = m(img.to(DEV))          # plain tensor input: the reference's detector branch
+    feat = _nchw_feat(m.native_plan(DEV), 3, 128, 96)
+    ref_boxes, ref_scores = O.person_detect(feat, sd, 256, 192, 0.3, 0.3, 5)
+    got = torch.stack([b.cpu() for b in out["boxes"]])
+    assert got.shape == (3, 5, 4)
+    np.testing.assert_allclose(out["box_scores"].cpu().numpy(), ref_scores.numpy(), atol=1e-5)
+    np.testing.assert_allclose(got.numpy(), ref_boxes.numpy(), atol=1e-4)
+    ref = O.forward(sd, {"image": img, "bboxes": got}, dual_head=True)
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
+    np.testing.assert_allclose(out["kh_keypoints"].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=1e-5)
+
+
 def test_predict_cli(tmp_path, capsys):
     """scripts/predict.py end to end: YAML config (grayscale 224), synthetic
     weights, a PNG and a YOLO label; printout format of the reference."""
