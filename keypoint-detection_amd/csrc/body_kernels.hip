@@ -18,15 +18,16 @@ namespace {
 __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img, int N, int Cin, int H,
                                                    int W, const float* __restrict__ w,
                                                    const float* __restrict__ b, float* __restrict__ out,
-                                                   int Ho, int Wo) {
+                                                   int Ho, int Wo, float* __restrict__ amax) {
   __shared__ float sw[16 * 27];
   __shared__ float sb[16];
+  __shared__ float red[4];
   const int nw = 16 * Cin * 9;
   for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = w[i];
   if (threadIdx.x < 16) sb[threadIdx.x] = b[threadIdx.x];
   __syncthreads();
   const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= N * Ho * Wo) return;
+  const bool live = pix < N * Ho * Wo;
   const int n = pix / (Ho * Wo), r = pix - n * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
   float in[27];
   for (int c = 0; c < Cin; ++c)
@@ -35,19 +36,32 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const int iy = oy * 2 - 1 + ky, ix = ox * 2 - 1 + kx;
-        in[c * 9 + ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
+        in[c * 9 + ky * 3 + kx] = (live && iy >= 0 && iy < H && ix >= 0 && ix < W)
                                       ? img[((size_t)(n * Cin + c) * H + iy) * W + ix] : 0.f;
       }
   float o[16];
+  float m_abs = 0.f;
 #pragma unroll
   for (int co = 0; co < 16; ++co) {
     float a = 0.f;
     for (int k = 0; k < Cin * 9; ++k) a = fmaf(in[k], sw[co * Cin * 9 + k], a);
     o[co] = kpd_act(a + sb[co], ACT_HSWISH);
+    m_abs = fmaxf(m_abs, fabsf(o[co]));
   }
-  float4* dst = reinterpret_cast<float4*>(out + (size_t)pix * 16);
+  if (live) {
+    float4* dst = reinterpret_cast<float4*>(out + (size_t)pix * 16);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    for (int q = 0; q < 4; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+  if (amax) {   // max|tap0| for the split FPN scale bound (conv_glds.hip)
+    const float wm = wave_max(live ? m_abs : 0.f);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (bm > 0.f) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(bm));
+    }
+  }
 }
 
 template <int K, int S>
@@ -84,7 +98,8 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ i
   *reinterpret_cast<float4*>(out + pix * Cp + q * 4) = o;
 }
 
-// One workgroup per image.  x: [N][HW][Cp]; w1: [sq][C]; w2: [C][sq].
+// One workgroup per image.  x: [N][HW][Cp]; w1 = fc1 transposed [C][sq];
+// w2 = fc2 transposed [sq][C] (C and sq are even in MobileNetV3-Small).
 __global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, int HW, int C, int Cp,
                                                  const float* __restrict__ w1, const float* __restrict__ b1,
                                                  const float* __restrict__ w2, const float* __restrict__ b2,
@@ -100,10 +115,25 @@ __global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, in
     const int q = tid % nq, pr = tid / nq;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (pr < rows) {
-      for (int p = pr; p < HW; p += rows) {
+      // 4 independent partial sums so four loads are in flight per thread
+      float4 s1 = s, s2 = s, s3 = s;
+      int p = pr;
+      for (; p + 3 * rows < HW; p += 4 * rows) {
+        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)p * Cp + q * 4);
+        const float4 b = *reinterpret_cast<const float4*>(xb + (size_t)(p + rows) * Cp + q * 4);
+        const float4 c = *reinterpret_cast<const float4*>(xb + (size_t)(p + 2 * rows) * Cp + q * 4);
+        const float4 d = *reinterpret_cast<const float4*>(xb + (size_t)(p + 3 * rows) * Cp + q * 4);
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+        s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
+        s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
+      }
+      for (; p < HW; p += rows) {
         const float4 v = *reinterpret_cast<const float4*>(xb + (size_t)p * Cp + q * 4);
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
+      s.x += s1.x + s2.x + s3.x; s.y += s1.y + s2.y + s3.y;
+      s.z += s1.z + s2.z + s3.z; s.w += s1.w + s2.w + s3.w;
     }
     part[tid] = s;
   }
@@ -119,16 +149,16 @@ __global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, in
     mean[tid * 4 + 2] = t.z / hw; mean[tid * 4 + 3] = t.w / hw;
   }
   __syncthreads();
-  // fc1 / fc2: one thread per output streaming its weight row with 16-byte
-  // loads (C and sq are multiples of 4 in MobileNetV3-Small), two partial sums.
+  // fc1 / fc2 as GEMVs over host-TRANSPOSED weights (w1t [C][sq], w2t [sq][C]):
+  // thread = output, lanes read consecutive outputs of one weight row, so
+  // every load instruction is one coalesced 256-B row segment and the loop
+  // carries no address dependence (deep load pipelining).
   for (int j = tid; j < sq; j += 256) {
-    const float4* wr = reinterpret_cast<const float4*>(w1 + (size_t)j * C);
     float a0 = 0.f, a1 = 0.f;
-#pragma unroll 4
-    for (int q = 0; q < C / 4; ++q) {
-      const float4 w = wr[q];
-      a0 = fmaf(w.x, mean[4 * q], a0); a1 = fmaf(w.y, mean[4 * q + 1], a1);
-      a0 = fmaf(w.z, mean[4 * q + 2], a0); a1 = fmaf(w.w, mean[4 * q + 3], a1);
+#pragma unroll 8
+    for (int c = 0; c < C; c += 2) {
+      a0 = fmaf(w1[(size_t)c * sq + j], mean[c], a0);
+      a1 = fmaf(w1[(size_t)(c + 1) * sq + j], mean[c + 1], a1);
     }
     hid[j] = fmaxf(a0 + a1 + b1[j], 0.f);
   }
@@ -136,17 +166,93 @@ __global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, in
   for (int c = tid; c < Cp; c += 256) {
     float v = 0.f;
     if (c < C) {
-      const float4* wr = reinterpret_cast<const float4*>(w2 + (size_t)c * sq);
       float a0 = 0.f, a1 = 0.f;
-#pragma unroll 4
-      for (int q = 0; q < sq / 4; ++q) {
-        const float4 w = wr[q];
-        a0 = fmaf(w.x, hid[4 * q], a0); a1 = fmaf(w.y, hid[4 * q + 1], a1);
-        a0 = fmaf(w.z, hid[4 * q + 2], a0); a1 = fmaf(w.w, hid[4 * q + 3], a1);
+#pragma unroll 8
+      for (int j = 0; j < sq; j += 2) {
+        a0 = fmaf(w2[(size_t)j * C + c], hid[j], a0);
+        a1 = fmaf(w2[(size_t)(j + 1) * C + c], hid[j + 1], a1);
       }
       v = kpd_hsigmoid(a0 + a1 + b2[c]);
     }
     scale[(size_t)n * Cp + c] = v;
+  }
+}
+
+// FPN lateral 1x1 conv with a small input width (cin_p <= 32) and 128 outputs,
+// plus the nearest-upsampled top-down residual (backbone.py:33-37) and the
+// max|out| the split16 FPN conv needs.  Pure streaming: one 16-byte store per
+// thread, weights transposed in LDS, the input pixel broadcast to the 32
+// threads that produce its 128 outputs.  64 pixels per workgroup.
+__global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __restrict__ in, int cin_p,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ res, int H, int W, int rh,
+                                                             int rw, int M, float* __restrict__ out,
+                                                             float* __restrict__ amax, const float* __restrict__ sc_in,
+                                                             float maxb, float maxs) {
+  __shared__ float sw[32 * 128];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  // split output (sc_in != null): x * 2^a_exp as f16 hi + lo, 32 channels per
+  // [hi32 | lo32] 128-byte group -- the K-tile row of the split FPN conv
+  float sa = 1.f;
+  if (sc_in) sa = ldexpf(1.f, split_a_exp(sc_in, maxb, maxs));
+  for (int i = tid; i < cin_p * 128; i += 256) {
+    const int co = i / cin_p, k = i - co * cin_p;
+    sw[k * 128 + co] = w[i];
+  }
+  __syncthreads();
+  const int c4 = tid & 31, sub = tid >> 5, co = c4 * 4;
+  const float4 b = *reinterpret_cast<const float4*>(bias + co);
+  const int HW = H * W;
+  const float sy = (float)rh / (float)H, sx = (float)rw / (float)W;
+  float m_abs = 0.f;
+  for (int it = 0; it < 8; ++it) {
+    const int m = blockIdx.x * 64 + it * 8 + sub;
+    if (m >= M) break;
+    const float* ip = in + (size_t)m * cin_p;
+    float4 acc = b;
+    for (int k = 0; k < cin_p; k += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(ip + k);
+      const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 wv = *reinterpret_cast<const float4*>(sw + (k + q) * 128 + co);
+        acc.x = fmaf(xs[q], wv.x, acc.x); acc.y = fmaf(xs[q], wv.y, acc.y);
+        acc.z = fmaf(xs[q], wv.z, acc.z); acc.w = fmaf(xs[q], wv.w, acc.w);
+      }
+    }
+    if (res) {
+      const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+      const int yy = rh == H ? y : min((int)floorf((float)y * sy), rh - 1);
+      const int xx = rw == W ? x : min((int)floorf((float)x * sx), rw - 1);
+      const float4 q = *reinterpret_cast<const float4*>(res + ((size_t)(n * rh + yy) * rw + xx) * 128 + co);
+      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+    }
+    m_abs = fmaxf(m_abs, fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fmaxf(fabsf(acc.z), fabsf(acc.w))));
+    if (sc_in) {
+      const float xs[4] = {acc.x * sa, acc.y * sa, acc.z * sa, acc.w * sa};
+      f16x4 hi, lo;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hi[q] = (_Float16)xs[q];
+        lo[q] = (_Float16)(xs[q] - (float)hi[q]);
+      }
+      _Float16* o16 = reinterpret_cast<_Float16*>(out) + (size_t)m * 256 + (co >> 5) * 64 + (co & 31);
+      *reinterpret_cast<f16x4*>(o16) = hi;
+      *reinterpret_cast<f16x4*>(o16 + 32) = lo;
+    } else {
+      *reinterpret_cast<float4*>(out + (size_t)m * 128 + co) = acc;
+    }
+  }
+  if (amax) {
+    const float wm = wave_max(m_abs);
+    if ((tid & 63) == 0) red[tid >> 6] = wm;
+    __syncthreads();
+    if (tid == 0) {
+      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (bm > 0.f) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(bm));
+    }
   }
 }
 
@@ -171,10 +277,10 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const float* __restr
 }  // namespace
 
 hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const float* w, const float* b,
-                       float* out, int Ho, int Wo, hipStream_t st) {
+                       float* out, int Ho, int Wo, float* amax, hipStream_t st) {
   const int total = N * Ho * Wo;
   hipLaunchKernelGGL(stem_kernel, dim3((total + 255) / 256), dim3(256), 0, st, img, N, Cin, H, W, w, b, out,
-                     Ho, Wo);
+                     Ho, Wo, amax);
   return hipGetLastError();
 }
 
@@ -196,6 +302,16 @@ hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* 
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st) {
   if (Cp > 1024 || sq > 256 || C % 4 || sq % 4) return hipErrorInvalidValue;
   hipLaunchKernelGGL(se_kernel, dim3(N), dim3(256), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
+                                 int N, int H, int W, int rh, int rw, void* out, float* amax, const float* sc_in,
+                                 float maxb, float maxs, hipStream_t st) {
+  if (cin_p > 32 || cin_p % 4) return hipErrorInvalidValue;
+  const int M = N * H * W;
+  hipLaunchKernelGGL(lateral_stream_kernel, dim3((M + 63) / 64), dim3(256), 0, st, in, cin_p, w, bias, res, H, W, rh,
+                     rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs);
   return hipGetLastError();
 }
 

@@ -23,8 +23,29 @@ struct EpiArgs {
   int act2, act3;
 };
 
-template <int BM, int BN>
-constexpr int epi_lds_bytes() { return BM * (BN + 4) * 4; }
+// Physical 16-byte chunk of logical chunk c in LDS row r (rows of CPR chunks):
+// an XOR swizzle that makes the MFMA fragment reads (ds_read_b128, 4 lane
+// groups of 16 on gfx950) and the staging writes bank-conflict free.
+template <int CPR>
+__device__ __forceinline__ int lds_chunk(int r, int c) {
+  if constexpr (CPR == 8) return c ^ (r & 7);
+  else if constexpr (CPR == 4) return c ^ ((r ^ (r >> 1)) & 3);
+  else return c;
+}
+
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
+// (block b and b+8 share one), so map the blocks of one XCD to CONSECUTIVE
+// logical tiles -- neighbouring implicit-GEMM tiles share 3x3 halo rows and
+// A tiles, which then hit the same 4 MiB L2.  Bijective for any nblk; a
+// placement other than round-robin only changes speed, never results.
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = b % 8, k = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// fp32 tile [BM][BN+4] plus the per-thread channel-statistics partials
+template <int BM, int BN, int NT = 256>
+constexpr int epi_lds_bytes() { return (BM * (BN + 4) + 2 * NT) * 4; }
 
 // acc[FM][FN] of wave (wm, wn) -> LDS tile [BM][BN+4] (fp32)
 template <int FM, int FN, int WM, int WN, int BN>
@@ -55,7 +76,8 @@ __device__ __forceinline__ void store4<__bf16>(__bf16* dst, const float4& v) {
 }
 
 // Requires a __syncthreads() between acc_to_lds and this call (done inside).
-template <typename TO, int BM, int BN>
+// NT = threads of the workgroup; LDS behind the tile holds 2*NT stats floats.
+template <typename TO, int BM, int BN, int NT = 256>
 __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0, int n0) {
   constexpr int P = BN + 4, C4 = BN / 4;
   const int tid = threadIdx.x;
@@ -63,7 +85,7 @@ __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0
   float amax = 0.f;
   TO* out = reinterpret_cast<TO*>(p.out);
   const int HW = p.H * p.W;
-  for (int idx = tid; idx < BM * C4; idx += 256) {
+  for (int idx = tid; idx < BM * C4; idx += NT) {
     const int row = idx / C4, c4 = idx - row * C4;
     const int m = m0 + row, co = n0 + c4 * 4;
     if (m >= p.M || co >= p.cout_p) continue;
@@ -100,13 +122,29 @@ __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0
     if ((tid & 63) == 0 && w > 0.f) atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(w));
   }
   if (p.stats) {
+    // column sums / maxima: NT/BN row groups in parallel, then one combine
+    constexpr int RG = NT / BN;
+    static_assert(RG >= 1 && BM % RG == 0, "stats layout");
+    float* part = tile + BM * P;
     __syncthreads();
-    if (tid < BN && n0 + tid < p.cout_p) {
+    {
+      const int col = tid % BN, rg = tid / BN;
       float s = 0.f, mx = -INFINITY;
-      for (int r = 0; r < BM; ++r) {
-        const float v = tile[r * P + tid];
+      for (int r = rg; r < BM; r += RG) {
+        const float v = tile[r * P + col];
         s += v;
         mx = fmaxf(mx, v);
+      }
+      part[rg * BN + col] = s;
+      part[NT + rg * BN + col] = mx;
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.cout_p) {
+      float s = part[tid], mx = part[NT + tid];
+#pragma unroll
+      for (int g = 1; g < RG; ++g) {
+        s += part[g * BN + tid];
+        mx = fmaxf(mx, part[NT + g * BN + tid]);
       }
       const int n = m0 / HW, t = (m0 - n * HW) / BM;
       float* st = p.stats + ((size_t)n * p.tiles_per_img + t) * 2 * p.cout_p;

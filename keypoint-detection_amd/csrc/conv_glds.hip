@@ -1,0 +1,279 @@
+// 16-bit-operand implicit-GEMM convolution with LDS-DMA staging (gfx950).
+//
+//   out[m, co] = act( scale * sum_k A[m, k] * Bw[co, k] + bias[co] )
+//   m = pixel (n, y, x) of an NHWC tensor, k = (tap, ci), tap = (ky, kx)
+//
+// Users (reference file:line):
+//   * FPN level-0 3x3 128->128 + BN + ReLU (dll/models/backbone.py:20-27,39),
+//     fp32-accurate "split" mode: every operand is carried as f16 hi + lo
+//     (x*s = hi + lo, power-of-two s) and each 16x16x32 k-step issues three
+//     v_mfma_f32_16x16x32_f16 (hi*lo, lo*hi, hi*hi) into one fp32 accumulator;
+//     f16 x f16 products are exact in fp32 and the dropped lo*lo term is
+//     ~2^-22 relative, so the result matches an fp32 conv to fp32 rounding.
+//     That keeps ChannelAttention's top-64 channel ORDER (keypoint_model.py:
+//     653-661) identical to the reference.
+//   * HeatmapHead 3x3 convs 64->256->256->64 (dll/models/heatmap_head.py:
+//     31-45,55-66) in bf16 ("mixed" precision), v_mfma_f32_16x16x32_bf16.
+//
+// Design (DESIGN.md "K6b"):
+//   * 512-thread workgroups (8 waves, 2 per SIMD at one workgroup per CU),
+//     BM = 256 pixels x BN in {64,128,256} output channels; every wave owns a
+//     (256/WAVES_M) x 64 tile of 16x16 fragments.
+//   * One K-tile = one 128-byte row per pixel / per output channel: 64 bf16
+//     input channels of one tap, or (split) 32 channels as [hi32 | lo32] f16
+//     -- the producer writes that interleaved layout, so staging is a pure copy.
+//   * Staging is LDS-DMA (buffer_load_dwordx4 ... lds): no VGPRs, no
+//     ds_write, no VALU conversion.  The 3x3 halo and the M tail come from the
+//     buffer descriptor's range check (an out-of-range offset loads zeros).
+//     The LDS image is XOR-swizzled (16-byte chunk c of row r at c ^ (r & 7),
+//     conflict-free ds_read_b128) by permuting the per-lane SOURCE chunk,
+//     because an LDS-DMA writes 1 KiB lane-linearly.
+//   * S-stage ring with a counted s_waitcnt vmcnt and a raw s_barrier: S-1
+//     K-tiles are in flight while the MFMAs of the current one run, and the
+//     single barrier per K-tile never drains the pipeline.
+//   * Epilogue: the accumulator tile is staged through LDS (conv_epilogue.h)
+//     for 16-byte row stores, fused bias / ReLU / unscale / channel sum+max.
+#include <algorithm>
+
+#include "kpd_common.h"
+#include "kpd_kernels.h"
+#include "conv_epilogue.h"
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, NT = 512, ROWB = 128;
+constexpr unsigned OOB = 0x80000000u;   // out-of-range voffset: the buffer load returns 0
+
+// one LDS-DMA wave-instruction: 16 bytes per lane from rsrc[voff + soff] to
+// (kept out of the kernel template: hipcc/ROCm 7.2 silently drops the host
+// stub of a template kernel that calls this builtin directly)
+// lds_dst + 16 * lane (lds_dst wave-uniform; out-of-range offsets load zeros)
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, char* lds_dst, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds_dst, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool SPLIT, typename TO, int KS, int BN, int S>
+__global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
+  constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
+  constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
+  constexpr int A_LD = 4, B_LD = BN / 64;          // LDS-DMA wave-instructions per K-tile per wave
+  constexpr int LPT = A_LD + B_LD;
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int EPI_BN = BN > 128 ? 128 : BN;
+  constexpr int EPI = epi_lds_bytes<BM, EPI_BN, NT>();
+  constexpr int LDS = S * STAGE > EPI ? S * STAGE : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(S >= 2 && (S - 2) * LPT < 64, "stages");
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int NTL = p.cout_p / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (L / NTL) * BM, n0 = (L % NTL) * BN;
+  const int H = p.H, W = p.W, HW = H * W, M = p.M;
+  const int cin_e = p.cin_e;
+
+  __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.in), (short)0, p.in_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rwt =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wt), (short)0, p.wt_bytes, 0x00020000);
+
+  // LDS-DMA geometry: one wave-instruction fills 8 rows x 128 B; lane l lands
+  // in row (l >> 3), physical chunk (l & 7), so it fetches logical chunk
+  // (l & 7) ^ (row & 7) of that row (rows start at multiples of 8).
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+  unsigned a_off[A_LD], a_taps[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int m = m0 + wave * 32 + i * 8 + lrow;
+    a_off[i] = 0;
+    a_taps[i] = 0;
+    if (m < M) {
+      const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+      a_off[i] = (unsigned)(m * p.in_cstride * 2 + lchunk * 16);
+#pragma unroll
+      for (int t = 0; t < KS * KS; ++t) {
+        const int yy = y + t / KS - KS / 2, xx = x + t % KS - KS / 2;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) a_taps[i] |= 1u << t;
+      }
+    }
+  }
+  unsigned b_off[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int co = n0 + wave * (BN / 8) + i * 8 + lrow;
+    b_off[i] = (unsigned)((co * KS * KS * cin_e) * 2 + lchunk * 16);
+  }
+  const int kc_per_tap = cin_e / 64;
+  const int KT = KS * KS * kc_per_tap;
+
+  // loader state (wave-uniform): next K-tile to issue as (tap, kc)
+  int ld_tap = 0, ld_kc = 0;
+  auto issue = [&](int stage) {
+    const int dy = ld_tap / KS - KS / 2, dx = ld_tap % KS - KS / 2;
+    const int delta = ((dy * W + dx) * p.in_cstride + ld_kc * 64) * 2;
+    char* sbase = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const unsigned voff = ((a_taps[i] >> ld_tap) & 1u) ? a_off[i] + delta : OOB;
+      glds16(rin, sbase + (wave * 32 + i * 8) * ROWB, voff, 0);
+    }
+    const int soff = (ld_tap * cin_e + ld_kc * 64) * 2;
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i)
+      glds16(rwt, sbase + (BM + wave * (BN / 8) + i * 8) * ROWB, b_off[i], soff);
+    if (++ld_kc == kc_per_tap) {
+      ld_kc = 0;
+      ++ld_tap;
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, r16 = lane & 15;
+  const int a_row = (wm * WM + r16) * ROWB, b_row = (BM + wn * 64 + r16) * ROWB;
+  auto chunk = [&](int c) { return ((c ^ (r16 & 7)) << 4); };
+  auto compute = [&](int stage) {
+    const char* sb = lds + stage * STAGE;
+    if constexpr (SPLIT) {
+      f16x8 ah[FM], al[FM], bh[FN], bl[FN];
+      const int ch = chunk(g), cl = chunk(4 + g);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        ah[i] = *reinterpret_cast<const f16x8*>(sb + a_row + i * 16 * ROWB + ch);
+        al[i] = *reinterpret_cast<const f16x8*>(sb + a_row + i * 16 * ROWB + cl);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        bh[j] = *reinterpret_cast<const f16x8*>(sb + b_row + j * 16 * ROWB + ch);
+        bl[j] = *reinterpret_cast<const f16x8*>(sb + b_row + j * 16 * ROWB + cl);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 av[FM], bv[FN];
+        const int c = chunk(ks * 4 + g);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(sb + a_row + i * 16 * ROWB + c);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(sb + b_row + j * 16 * ROWB + c);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- S-stage ring: tile k lives in stage k % S ----
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < KT) issue(s);
+  int cs = 0;                 // stage of the tile being computed
+  int is = S - 1;             // stage the next issue writes
+  for (int kt = 0; kt < KT; ++kt) {
+    // tile kt has landed once at most the tiles issued after it are pending
+    if (kt + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();   // tile kt visible to all; stage of tile kt-1 free
+    asm volatile("" ::: "memory");
+    if (kt + S - 1 < KT) issue(is);
+    compute(cs);
+    cs = cs + 1 == S ? 0 : cs + 1;
+    is = is + 1 == S ? 0 : is + 1;
+  }
+  __syncthreads();   // every wave's last LDS read done before the epilogue reuses LDS
+
+  // ---------------- epilogue ----------------
+  float scale = 1.f;
+  if constexpr (SPLIT) scale = ldexpf(1.f, -(split_a_exp(p.sc_in, p.sc_maxb, p.sc_maxs) + p.w_exp));
+  EpiArgs e;
+  e.bias = p.bias; e.out = p.out; e.res = nullptr; e.stats = p.stats; e.amax = nullptr; e.scale = scale;
+  e.M = M; e.H = H; e.W = W; e.cout_p = p.cout_p; e.out_cstride = p.out_cstride; e.rh = H; e.rw = W;
+  e.act = p.act; e.tiles_per_img = p.tiles_per_img;
+  e.post_scale = nullptr; e.post_shift = nullptr; e.act2 = 0; e.act3 = 0;
+  float* tile = reinterpret_cast<float*>(lds);
+  constexpr int HALVES = BN / EPI_BN, WN_PER = EPI_BN / 64;
+#pragma unroll
+  for (int h = 0; h < HALVES; ++h) {
+    if (h) __syncthreads();
+    if (wn / WN_PER == h) acc_to_lds<FM, FN, WM, 64, EPI_BN>(tile, acc, wm, wn % WN_PER, lane);
+    tile_store<TO, BM, EPI_BN, NT>(tile, e, m0, n0 + h * EPI_BN);
+  }
+}
+
+constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
+
+template <bool SPLIT, typename TO, int KS, int BN, int S>
+hipError_t launch(const Conv16Args& a0, hipStream_t st) {
+  constexpr long OS = sizeof(TO);
+  Conv16Args a = a0;
+  const long wt_bytes = (long)a.cout_p * KS * KS * a.cin_e * 2;
+  const long HW = (long)a.H * a.W;
+  const long img_bytes = HW * a.in_cstride * 2;
+  if (wt_bytes > kMaxDesc || img_bytes > kMaxDesc) return hipErrorInvalidValue;
+  a.wt_bytes = (int)wt_bytes;
+  const int chunk = (int)std::min<long>(a.N, kMaxDesc / img_bytes);
+  for (int n0 = 0; n0 < a0.N; n0 += chunk) {
+    const int nb = std::min(chunk, a0.N - n0);
+    a.N = nb;
+    a.M = (int)(nb * HW);
+    a.in = static_cast<const char*>(a0.in) + n0 * img_bytes;
+    a.out = static_cast<char*>(a0.out) + n0 * HW * a.out_cstride * OS;
+    a.stats = a0.stats ? a0.stats + (long)n0 * a.tiles_per_img * 2 * a.cout_p : nullptr;
+    a.in_bytes = (int)(nb * img_bytes);
+    dim3 grid(((a.M + BM - 1) / BM) * (a.cout_p / BN));
+    hipLaunchKernelGGL((conv16_kernel<SPLIT, TO, KS, BN, S>), grid, dim3(NT), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+int conv16_tile_m() { return BM; }
+
+hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.cin_e % 64 != 0 || a.in_cstride % 8 != 0 || (a.stats && (a.H * a.W) % BM != 0))
+    return hipErrorInvalidValue;
+  if (split) {
+    if (out_bf16 || a.cout_p != 128 || !a.sc_in) return hipErrorInvalidValue;
+    return launch<true, float, 3, 128, 3>(a, st);
+  }
+  if (a.cout_p % 256 == 0)
+    return out_bf16 ? launch<false, __bf16, 3, 256, 2>(a, st) : launch<false, float, 3, 256, 2>(a, st);
+  if (a.cout_p % 128 == 0)
+    return out_bf16 ? launch<false, __bf16, 3, 128, 3>(a, st) : launch<false, float, 3, 128, 3>(a, st);
+  if (a.cout_p % 64 == 0)
+    return out_bf16 ? launch<false, __bf16, 3, 64, 3>(a, st) : launch<false, float, 3, 64, 3>(a, st);
+  return hipErrorInvalidValue;
+}

@@ -26,105 +26,121 @@
 //   * Epilogue fuses bias (BN folded on the host), activation, residual add
 //     with optional nearest-upsample indexing (FPN top-down), per-image
 //     channel sum/max partials (ChannelAttention pooling), bf16/fp32 stores.
+#include <algorithm>
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 #include "conv_epilogue.h"
 
 namespace {
 
-template <typename TA, typename TO, int KS, int BM, int BN, int BK>
+template <typename TA, typename TO, int KS, int BM, int BN, int BK, bool PF2 = false>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(TA);
   constexpr int ROWB = BK * ES;           // bytes of one LDS row (one K-tile of one row)
   constexpr int CPR = ROWB / 16;          // 16-byte chunks per row
-  constexpr int LDSROW = ROWB + 16;       // padded row pitch (bank spread)
+  constexpr int LDSROW = ROWB;            // unpadded; 16-B chunks XOR-swizzled (lds_chunk)
   constexpr int EPC = 16 / ES;            // elements per chunk
   constexpr int A_TOT = BM * CPR, B_TOT = BN * CPR;
   constexpr int NA = (A_TOT + 255) / 256, NB = (B_TOT + 255) / 256;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int KSTEPS = ROWB / 64;       // 4 lane groups x 16 B per k-step
+  constexpr int BUF_A = BM * LDSROW, BUF_B = BN * LDSROW;
+  constexpr unsigned OOB = 0x80000000u;   // out-of-range voffset: the buffer load returns 0
   static_assert(FM >= 1 && FN >= 1, "tile too small");
   static_assert(ROWB % 64 == 0, "BK must cover 64 bytes");
 
-  constexpr int MAIN_LDS = 2 * (BM + BN) * LDSROW;
+  constexpr int MAIN_LDS = 2 * (BUF_A + BUF_B);
   constexpr int EPI_LDS = epi_lds_bytes<BM, BN>();
   __shared__ __attribute__((aligned(16))) char lds[MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS];
   char* As = lds;
-  char* Bs = lds + 2 * BM * LDSROW;
+  char* Bs = lds + 2 * BUF_A;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // 1-D grid: N-tile fastest (N-tiles of one M-tile share the A tile), XCD-aware order
+  const int NT = (p.cout_p + BN - 1) / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (L / NT) * BM, n0 = (L % NT) * BN;
   const int H = p.H, W = p.W, HW = H * W, M = p.M;
   const int cin_p = p.cin_p, cout_p = p.cout_p;
-  const TA* __restrict__ in = reinterpret_cast<const TA*>(p.in);
-  const TA* __restrict__ wt = reinterpret_cast<const TA*>(p.wt);
 
-  // Pixel coordinates of the A rows this thread stages (fixed over K).
-  int a_n[NA], a_y[NA], a_x[NA];
+  // Buffer descriptors (wave-uniform kernargs): 32-bit offsets, hardware range
+  // check -> halo / tail lanes get 0 without a branch (T8/T20 of the guide).
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.in), (short)0,
+                                                                       p.in_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwt = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wt), (short)0,
+                                                                       p.wt_bytes, 0x00020000);
+
+  // Per-thread staging geometry, fixed over K: byte offsets into the input /
+  // weight buffers and the LDS slot of each 16-byte chunk this thread moves.
+  unsigned a_off[NA];
+  int a_scale_off[NA];
+  unsigned a_taps[NA];                    // bit t: tap t of the KSxKS window is inside the image
+  int a_lds[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int c = tid + 256 * i;
-    const int m = m0 + c / CPR;
+    const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
+    const int m = m0 + row;
+    a_lds[i] = row * LDSROW + lds_chunk<CPR>(row, col) * 16;
+    a_taps[i] = 0;
+    a_off[i] = 0;
+    a_scale_off[i] = 0;
     if (c < A_TOT && m < M) {
-      const int n = m / HW, r = m - n * HW, y = r / W;
-      a_n[i] = n; a_y[i] = y; a_x[i] = r - y * W;
-    } else {
-      a_n[i] = -1; a_y[i] = 0; a_x[i] = 0;
+      const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+      a_off[i] = (unsigned)(((n * H + y) * W + x) * p.in_cstride + col * EPC) * ES;
+      a_scale_off[i] = n * cin_p + col * EPC;
+#pragma unroll
+      for (int t = 0; t < KS * KS; ++t) {
+        const int yy = y + t / KS - KS / 2, xx = x + t % KS - KS / 2;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) a_taps[i] |= 1u << t;
+      }
     }
+  }
+  unsigned b_off[NB];
+  int b_lds[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
+    const int co = n0 + row;
+    b_lds[i] = row * LDSROW + lds_chunk<CPR>(row, col) * 16;
+    b_off[i] = (c < B_TOT && co < cout_p) ? (unsigned)((co * KS * KS * cin_p + col * EPC) * ES) : OOB;
   }
 
   const int kc_per_tap = cin_p / BK;
   const int KT = KS * KS * kc_per_tap;
-  uint4 ra[NA], rb[NB];
+  // two register stage sets: with PF2 tile k+2 is in flight while tile k is computed
+  uint4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
 
-  auto load_tile = [&](int kt) {
-    const int tap = kt / kc_per_tap;
+  auto load_tile = [&](int kt, uint4 (&ra)[NA], uint4 (&rb)[NB]) {
+    const int tap = kt / kc_per_tap;                       // wave-uniform (SALU)
     const int ci0 = (kt - tap * kc_per_tap) * BK;
-    const int dy = tap / KS - KS / 2, dx = tap % KS - KS / 2;
+    const int delta = (((tap / KS - KS / 2) * W + (tap % KS - KS / 2)) * p.in_cstride + ci0) * ES;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int c = tid + 256 * i, col = c % CPR;
-      const int yy = a_y[i] + dy, xx = a_x[i] + dx;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (a_n[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const int ci = ci0 + col * EPC;
-        const TA* src = in + ((size_t)(a_n[i] * H + yy) * W + xx) * p.in_cstride + ci;
-        v = *reinterpret_cast<const uint4*>(src);
-        if constexpr (sizeof(TA) == 4) {
-          if (p.a_scale) {  // SE excitation folded into the project conv's A load
-            const float4 s = *reinterpret_cast<const float4*>(p.a_scale + (size_t)a_n[i] * cin_p + ci);
-            float4 f = *reinterpret_cast<float4*>(&v);
-            f.x *= s.x; f.y *= s.y; f.z *= s.z; f.w *= s.w;
-            v = *reinterpret_cast<uint4*>(&f);
-          }
+      const unsigned voff = ((a_taps[i] >> tap) & 1u) ? a_off[i] + delta : OOB;
+      uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rin, voff, 0, 0));
+      if constexpr (sizeof(TA) == 4) {
+        if (p.a_scale) {  // SE excitation folded into the project conv's A load
+          const float4 s = *reinterpret_cast<const float4*>(p.a_scale + a_scale_off[i] + ci0);
+          float4 f = __builtin_bit_cast(float4, v);
+          f.x *= s.x; f.y *= s.y; f.z *= s.z; f.w *= s.w;
+          v = __builtin_bit_cast(uint4, f);
         }
       }
       ra[i] = v;
     }
+    const int soff = (tap * cin_p + ci0) * ES;              // scalar offset
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
-      const int co = n0 + row;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (c < B_TOT && co < cout_p)
-        v = *reinterpret_cast<const uint4*>(wt + ((size_t)co * KS * KS + tap) * cin_p + ci0 + col * EPC);
-      rb[i] = v;
-    }
+    for (int i = 0; i < NB; ++i)
+      rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwt, b_off[i], soff, 0));
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[NA], const uint4 (&rb)[NB]) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int c = tid + 256 * i;
-      if (c < A_TOT)
-        *reinterpret_cast<uint4*>(As + (buf * BM + c / CPR) * LDSROW + (c % CPR) * 16) = ra[i];
-    }
+    for (int i = 0; i < NA; ++i)
+      if (A_TOT % 256 == 0 || tid + 256 * i < A_TOT) *reinterpret_cast<uint4*>(As + buf * BUF_A + a_lds[i]) = ra[i];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int c = tid + 256 * i;
-      if (c < B_TOT)
-        *reinterpret_cast<uint4*>(Bs + (buf * BN + c / CPR) * LDSROW + (c % CPR) * 16) = rb[i];
-    }
+    for (int i = 0; i < NB; ++i)
+      if (B_TOT % 256 == 0 || tid + 256 * i < B_TOT) *reinterpret_cast<uint4*>(Bs + buf * BUF_B + b_lds[i]) = rb[i];
   };
 
   f32x4 acc[FM][FN];
@@ -134,23 +150,19 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, r16 = lane & 15;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_tile(kt + 1);
-    const char* Ab = As + (cur * BM + wm * WM + r16) * LDSROW;
-    const char* Bb = Bs + (cur * BN + wn * WN + r16) * LDSROW;
+  const char* Abase = As + (wm * WM + r16) * LDSROW;
+  const char* Bbase = Bs + (wn * WN + r16) * LDSROW;
+  auto compute = [&](int cur) {
+    const char* Ab = Abase + cur * BUF_A;
+    const char* Bb = Bbase + cur * BUF_B;
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int ch = lds_chunk<CPR>(r16, ks * 4 + g) * 16;   // row & 7 == r16 & 7
       uint4 av[FM], bv[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        av[i] = *reinterpret_cast<const uint4*>(Ab + i * 16 * LDSROW + (ks * 4 + g) * 16);
+      for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const uint4*>(Ab + i * 16 * LDSROW + ch);
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bv[j] = *reinterpret_cast<const uint4*>(Bb + j * 16 * LDSROW + (ks * 4 + g) * 16);
+      for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const uint4*>(Bb + j * 16 * LDSROW + ch);
       if constexpr (sizeof(TA) == 4) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -168,12 +180,45 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                *reinterpret_cast<const bf16x8*>(&av[i]), *reinterpret_cast<const bf16x8*>(&bv[j]),
-                acc[i][j], 0, 0, 0);
+                __builtin_bit_cast(bf16x8, av[i]), __builtin_bit_cast(bf16x8, bv[j]), acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < KT) store_tile(cur ^ 1);
+  };
+
+  // LDS buffer (k & 1) holds K-tile k.  One MFMA site in the loop keeps the
+  // accumulators in a single AGPR home (a 2x-unrolled loop made the register
+  // allocator rotate them through VGPRs every iteration).
+  if constexpr (PF2) {   // latency-bound small GEMMs: two tiles in flight
+    load_tile(0, ra0, rb0);
+    store_tile(0, ra0, rb0);
+    if (KT > 1) load_tile(1, ra1, rb1);
     __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cur = kt & 1;
+      // ra0 holds tile kt+1 (odd kt) or is free (even kt) -- swap roles by parity
+      if (cur == 0) {
+        if (kt + 2 < KT) load_tile(kt + 2, ra0, rb0);
+      } else {
+        if (kt + 2 < KT) load_tile(kt + 2, ra1, rb1);
+      }
+      compute(cur);
+      if (kt + 1 < KT) {
+        if (cur == 0) store_tile(1, ra1, rb1);
+        else store_tile(0, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  } else {               // MFMA-bound convs: one register set keeps 2 waves/SIMD
+    load_tile(0, ra0, rb0);
+    store_tile(0, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < KT) load_tile(kt + 1, ra0, rb0);
+      compute(cur);
+      if (kt + 1 < KT) store_tile(cur ^ 1, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // ---------------- epilogue (LDS-staged, 16-byte row stores) ----------------
@@ -187,11 +232,35 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   tile_store<TO, BM, BN>(tile, e, m0, n0);
 }
 
-template <typename TA, typename TO, int KS, int BM, int BN, int BK>
-hipError_t launch(const ConvArgs& a, hipStream_t st) {
-  dim3 grid((a.M + BM - 1) / BM, (a.cout_p + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_mfma_kernel<TA, TO, KS, BM, BN, BK>), grid, dim3(256), 0, st, a);
-  return hipGetLastError();
+constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
+
+template <typename TA, typename TO, int KS, int BM, int BN, int BK, bool PF2 = false>
+hipError_t launch(const ConvArgs& a0, hipStream_t st) {
+  constexpr long ES = sizeof(TA), OS = sizeof(TO);
+  ConvArgs a = a0;
+  const long wt_bytes = (long)a.cout_p * KS * KS * a.cin_p * ES;
+  const long img_bytes = (long)a.H * a.W * a.in_cstride * ES;
+  if (wt_bytes > kMaxDesc || img_bytes > kMaxDesc) return hipErrorInvalidValue;
+  a.wt_bytes = (int)wt_bytes;
+  // images per launch so the input descriptor stays below 2^31 bytes
+  const int chunk = (int)std::min<long>(a.N, kMaxDesc / img_bytes);
+  const long HW = (long)a.H * a.W;
+  for (int n0 = 0; n0 < a0.N; n0 += chunk) {
+    const int nb = std::min(chunk, a0.N - n0);
+    a.N = nb;
+    a.M = (int)(nb * HW);
+    a.in = static_cast<const char*>(a0.in) + n0 * img_bytes;
+    a.out = static_cast<char*>(a0.out) + n0 * HW * a.out_cstride * OS;
+    a.res = a0.res ? a0.res + n0 * (long)a.rh * a.rw * a.cout_p : nullptr;
+    a.a_scale = a0.a_scale ? a0.a_scale + (long)n0 * a.cin_p : nullptr;
+    a.stats = a0.stats ? a0.stats + (long)n0 * a.tiles_per_img * 2 * a.cout_p : nullptr;
+    a.in_bytes = (int)(nb * img_bytes);
+    dim3 grid(((a.M + BM - 1) / BM) * ((a.cout_p + BN - 1) / BN));
+    hipLaunchKernelGGL((conv_mfma_kernel<TA, TO, KS, BM, BN, BK, PF2>), grid, dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace
@@ -213,11 +282,11 @@ hipError_t launch_conv(const ConvArgs& a, ConvDType dt, int ks, hipStream_t st) 
     // grid covers the 256 CUs at least twice
     const long blocks128 = (long)((a.M + 127) / 128) * ((a.cout_p + 127) / 128);
     if (blocks128 < 512 && a.stats == nullptr) {
-      if (a.cout_p <= 32) return bk32 ? launch<float, float, 1, 64, 32, 32>(a, st)
-                                      : launch<float, float, 1, 64, 32, 16>(a, st);
-      if (a.cout_p <= 64) return bk32 ? launch<float, float, 1, 64, 64, 32>(a, st)
-                                      : launch<float, float, 1, 64, 64, 16>(a, st);
-      return bk32 ? launch<float, float, 1, 64, 128, 32>(a, st) : launch<float, float, 1, 64, 128, 16>(a, st);
+      if (a.cout_p <= 32) return bk32 ? launch<float, float, 1, 64, 32, 32, true>(a, st)
+                                      : launch<float, float, 1, 64, 32, 16, true>(a, st);
+      if (a.cout_p <= 64) return bk32 ? launch<float, float, 1, 64, 64, 32, true>(a, st)
+                                      : launch<float, float, 1, 64, 64, 16, true>(a, st);
+      return bk32 ? launch<float, float, 1, 64, 128, 32, true>(a, st) : launch<float, float, 1, 64, 128, 16, true>(a, st);
     }
     if (a.cout_p <= 32) return bk32 ? launch<float, float, 1, 128, 32, 32>(a, st)
                                     : launch<float, float, 1, 128, 32, 16>(a, st);

@@ -6,6 +6,7 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 enum KpdAct : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2, ACT_HSWISH = 3, ACT_SIGMOID = 4 };
 
@@ -33,6 +34,19 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// Split (fp32-accurate f16 hi+lo) FPN level 0: power-of-two activation
+// exponent from the device-side bound U >= max|lateral0| (producer and
+// consumer evaluate the same expression on the same inputs, so they agree):
+// U = (maxb + max|tap0| * maxs + max|lateral1|) * (1 + 2^-7), a_exp = 14 - e
+// with U < 2^e, hence max|x * 2^a_exp| < 2^14 and the f16 hi part is finite.
+__device__ __forceinline__ int split_a_exp(const float* sc_in, float maxb, float maxs) {
+  const float u = (maxb + sc_in[0] * maxs + sc_in[1]) * 1.0078125f;
+  if (!(u > 0.f) || !(u < INFINITY)) return 0;
+  int e;
+  frexpf(u, &e);
+  return min(max(14 - e, -100), 100);
 }
 
 #define KPD_CHECK_LAUNCH() (hipGetLastError())

@@ -22,20 +22,28 @@ struct ConvArgs {
   const float* post_scale;  // optional second affine after act (see conv_epilogue.h)
   const float* post_shift;
   int act2, act3;
+  int in_bytes, wt_bytes;   // buffer-descriptor extents; filled by launch_conv (each < 2^31)
 };
 
-// FPN level-0 3x3 conv on the f16 MFMA pipe with hi/lo operand split (conv_split16.hip)
-struct Split16Args {
-  const float* in;       // NHWC [N][H][W][cin] f32 (lateral 0)
-  const _Float16* w_hi;  // [cout_p][9][cin], BN-folded, scaled by 2^w_exp
-  const _Float16* w_lo;
+// 16-bit-operand 3x3 conv with LDS-DMA staging (conv_glds.hip): bf16 operands,
+// or "split" f16 hi|lo operands (fp32-accurate, FPN level 0).
+struct Conv16Args {
+  const void* in;        // NHWC [N][H][W][in_cstride] 16-bit; split: per 32 channels [hi32|lo32]
+  const void* wt;        // [cout_p][9][cin_e] 16-bit (BN folded; split: same interleave, scaled 2^w_exp)
   const float* bias;     // [cout_p]
-  float* out;            // NHWC [N][H][W][cout_p]
-  float* stats;          // [N][tiles_per_img][2][cout_p] or null
-  const float* amax;     // device max|in| (published by the lateral conv)
-  int N, H, W, cin, cout_p, act, M, tiles_per_img, w_exp;
+  void* out;             // NHWC [N][H][W][out_cstride] (f32 or bf16)
+  float* stats;          // optional [N][tiles_per_img][2][cout_p] (H*W % 256 == 0)
+  int N, H, W;
+  int cin_e;             // 16-bit elements per tap row (cin, or 2*cin in split mode), % 64 == 0
+  int cout_p, in_cstride, out_cstride, act, M, tiles_per_img;
+  // split mode: activation scale from the bound max|A| <= maxb + sc_in[0]*maxs + sc_in[1]
+  const float* sc_in;
+  float sc_maxb, sc_maxs;
+  int w_exp;
+  int in_bytes, wt_bytes;   // filled by the launcher
 };
-hipError_t launch_conv3x3_split16(const Split16Args& a, hipStream_t st);
+hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st);
+int conv16_tile_m();
 
 enum ConvDType : int { CONV_F32 = 0, CONV_BF16_OUT_BF16 = 1, CONV_BF16_OUT_F32 = 2 };
 
@@ -44,13 +52,17 @@ hipError_t launch_conv(const ConvArgs& a, ConvDType dt, int ks, hipStream_t st);
 
 // ---- MobileNetV3 body (body_kernels.hip) ----
 hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const float* w, const float* b,
-                       float* out, int Ho, int Wo, hipStream_t st);
+                       float* out, int Ho, int Wo, float* amax, hipStream_t st);
 hipError_t launch_dwconv(const float* in, const float* w, const float* b, float* out, int N, int H, int W,
                          int Cp, int Ho, int Wo, int k, int s, int act, hipStream_t st);
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st);
+// sc_in != null: split output (f16 [hi32|lo32] groups, scale from split_a_exp)
+hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
+                                 int N, int H, int W, int rh, int rw, void* out, float* amax, const float* sc_in,
+                                 float maxb, float maxs, hipStream_t st);
 
 // ---- channel attention / ROI / heatmap head / decode (head_kernels.hip) ----
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,

@@ -107,7 +107,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   void* h2 = nullptr;
   float* h3 = nullptr;
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
-  float* amax = nullptr;  // max|lateral0| for the split16 FPN conv scale
+  float* sc = nullptr;    // split FPN scale inputs: [max|tap0|, max|lateral1|]
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
   float* pd_head = nullptr;     // [B][56*56][48]
@@ -150,7 +150,11 @@ struct kpd_plan {
   float *hca_w0 = nullptr, *hca_b0 = nullptr, *hca_w2 = nullptr, *hca_b2 = nullptr;
   float *sa_w = nullptr, *sa_b = nullptr;
   DevConv hm1, hm2, hm3;
-  struct { _Float16 *hi = nullptr, *lo = nullptr; int w_exp = 0; } fpn0s;  // split16 weights
+  struct {
+    _Float16* hl = nullptr;   // [128][9][4][hi32|lo32]
+    int w_exp = 0;
+    float maxb = 0.f, maxs = 0.f;
+  } fpn0s;  // split FPN level-0 weights
   float *fin_w = nullptr, *fin_b = nullptr;
   float* zero_bias = nullptr;  // 128 zeros for bias-free laterals
   // person-detector glue: box_heads[0] ++ cls_heads[0] as one 1x1 conv (45 -> 48 ch)
@@ -281,6 +285,17 @@ int pack_dw(kpd_plan* p, const std::string& pre, int k, int s, int act, DevDW& d
   return upload(p, pb, &dw.b);
 }
 
+// [rows][cols] (a 1x1 conv / linear weight) -> uploaded as [cols][rows]
+int pack_transposed(kpd_plan* p, const std::string& name, int rows, int cols, float** out, std::string& missing) {
+  const HostT* w = get(p, name, missing);
+  if (!w) return KPD_ESTATE;
+  if (w->data.size() != (size_t)rows * cols) return fail(KPD_EINVAL, "bad size for " + name);
+  std::vector<float> t((size_t)rows * cols);
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) t[(size_t)c * rows + r] = w->data[(size_t)r * cols + c];
+  return upload(p, t, out);
+}
+
 // BatchNorm as a per-channel affine (scale, shift), padded to cout_p -- for a
 // BN that sits behind a non-linearity and cannot be folded into a conv.
 int pack_bn_affine(kpd_plan* p, const std::string& bn, int cout_p, float** s_out, float** t_out,
@@ -304,10 +319,17 @@ int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& m
   return upload(p, w->data, out);
 }
 
-// Split16 weights for the FPN level-0 conv: downloads the packed fp32 weights
-// [cout_p][9][cin_p], scales by 2^w_exp so max|w| < 2^15, splits into f16 hi/lo.
-int pack_split16(kpd_plan* p, const DevConv& dc) {
-  const size_t n = (size_t)dc.cout_p * 9 * dc.cin_p;
+// Split weights for the FPN level-0 conv: downloads the packed fp32 weights
+// [cout_p][9][cin_p], scales by 2^w_exp so max|w| < 2^15 and splits every value
+// into f16 hi + lo, stored per 32 input channels as [hi32 | lo32] (the 128-byte
+// K-tile row of conv_glds.hip).  Also derives the constants of the device-side
+// bound max|lateral0| <= maxb + max|tap0| * maxs + max|lateral1| that fixes the
+// activation scale before lateral 0 is written (backbone.py:33-37: lateral0 =
+// conv1x1(tap0) + up(lateral1)).
+int pack_split16(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
+  const int cin = dc.cin_p;
+  if (cin % 32 != 0) return fail(KPD_EINVAL, "split FPN conv needs cin % 32 == 0");
+  const size_t n = (size_t)dc.cout_p * 9 * cin;
   std::vector<float> w(n);
   HIP_TRY(hipMemcpy(w.data(), dc.w, n * sizeof(float), hipMemcpyDeviceToHost));
   float mx = 0.f;
@@ -315,15 +337,30 @@ int pack_split16(kpd_plan* p, const DevConv& dc) {
   int e = 0;
   if (mx > 0.f) std::frexp(mx, &e);
   const int w_exp = std::min(std::max(14 - e, -100), 100);
-  std::vector<_Float16> hi(n), lo(n);
-  for (size_t i = 0; i < n; ++i) {
-    const float x = std::ldexp(w[i], w_exp);
-    hi[i] = (_Float16)x;
-    lo[i] = (_Float16)(x - (float)hi[i]);
-  }
-  if (int rc = upload(p, hi, &p->fpn0s.hi)) return rc;
-  if (int rc = upload(p, lo, &p->fpn0s.lo)) return rc;
+  std::vector<_Float16> hl(2 * n);
+  for (size_t row = 0; row < (size_t)dc.cout_p * 9; ++row)
+    for (int ci = 0; ci < cin; ++ci) {
+      const float x = std::ldexp(w[row * cin + ci], w_exp);
+      const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+      const size_t o = row * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
+      hl[o] = hi;
+      hl[o + 32] = lo;
+    }
+  if (int rc = upload(p, hl, &p->fpn0s.hl)) return rc;
   p->fpn0s.w_exp = w_exp;
+  // lateral-0 bound constants (1x1 conv, [cout_p][cin_p] fp32 + bias)
+  std::vector<float> lw((size_t)lat0.cout_p * lat0.cin_p), lb(lat0.cout_p);
+  HIP_TRY(hipMemcpy(lw.data(), lat0.w, lw.size() * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(lb.data(), lat0.b, lb.size() * sizeof(float), hipMemcpyDeviceToHost));
+  double maxb = 0.0, maxs = 0.0;
+  for (int co = 0; co < lat0.cout_p; ++co) {
+    double sa = 0.0;
+    for (int ci = 0; ci < lat0.cin_p; ++ci) sa += std::fabs((double)lw[(size_t)co * lat0.cin_p + ci]);
+    maxs = std::max(maxs, sa);
+    maxb = std::max(maxb, std::fabs((double)lb[co]));
+  }
+  p->fpn0s.maxb = (float)(maxb * (1.0 + 1e-6));
+  p->fpn0s.maxs = (float)(maxs * (1.0 + 1e-6));
   return KPD_OK;
 }
 
@@ -358,7 +395,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   for (int i = 0; i < 4; ++i) w.lat[i] = c.take<float>((size_t)B * lh[i] * lw[i] * 128);
   w.feat = c.take<float>((size_t)B * d.Hf * d.Wf * 128);
   w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
-  w.amax = c.take<float>(1);
+  w.sc = c.take<float>(2);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
@@ -453,6 +490,19 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
   return KPD_OK;
 }
 
+// HeatmapHead 3x3 conv + bias + BN + ReLU on the 56x56 ROI maps: bf16 weights
+// go to the LDS-DMA kernel (conv_glds.hip), fp32 to the generic one.
+// out_kind: 1 = bf16 output, 2 = fp32 output (bf16 weights); fp32 otherwise.
+int hm_conv(const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind, hipStream_t st) {
+  if (!L.bf16) return conv(L, in, R, 56, 56, in_cstride, out, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
+  Conv16Args a{};
+  a.in = in; a.wt = L.w; a.bias = L.b; a.out = out;
+  a.N = R; a.H = 56; a.W = 56; a.cin_e = L.cin_p; a.cout_p = L.cout_p; a.in_cstride = in_cstride;
+  a.out_cstride = L.cout_p; a.act = ACT_RELU; a.M = R * 56 * 56;
+  HIP_TRY(launch_conv16(a, 0, out_kind == 1, st));
+  return KPD_OK;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -505,7 +555,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   HIP_TRY(hipSetDevice(p->device));
   for (void* a : p->allocs) (void)hipFree(a);
   p->allocs.clear();
-  p->fpn0s.hi = p->fpn0s.lo = nullptr;
+  p->fpn0s.hl = nullptr;
   p->pd = DevConv();
   p->anchors = nullptr;
   p->kh_ds1 = DevConv();
@@ -555,9 +605,9 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     if (bn.cfg.se) {
       const std::string s = pre + std::to_string(j);
       bn.se.C = bn.cfg.exp; bn.se.Cp = pad16(bn.cfg.exp); bn.se.sq = se_squeeze(bn.cfg.exp);
-      chk(pack_plain(p, s + ".fc1.weight", &bn.se.w1, missing, (size_t)bn.se.sq * bn.se.C));
+      chk(pack_transposed(p, s + ".fc1.weight", bn.se.sq, bn.se.C, &bn.se.w1, missing));
       chk(pack_plain(p, s + ".fc1.bias", &bn.se.b1, missing, bn.se.sq));
-      chk(pack_plain(p, s + ".fc2.weight", &bn.se.w2, missing, (size_t)bn.se.sq * bn.se.C));
+      chk(pack_transposed(p, s + ".fc2.weight", bn.se.C, bn.se.sq, &bn.se.w2, missing));
       chk(pack_plain(p, s + ".fc2.bias", &bn.se.b2, missing, bn.se.C));
       ++j;
     }
@@ -570,7 +620,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
-  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_split16(p, p->fpn0));
+  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_split16(p, p->fpn0, p->lat[0]));
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
@@ -714,7 +764,8 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
     d.w[i + 1] = (d.w[i] + 2 * pd - k) / s + 1;
   }
   d.Hf = d.h[0]; d.Wf = d.w[0];
-  const int HWf = d.Hf * d.Wf, TM = conv_tile_m();
+  const bool split = p->precision == KPD_PRECISION_MIXED && p->fpn0s.hl != nullptr;
+  const int HWf = d.Hf * d.Wf, TM = split ? conv16_tile_m() : conv_tile_m();
   d.fused_stats = (HWf % TM) == 0;
   d.tiles = d.fused_stats ? HWf / TM : std::min(64, HWf);
   if (int rc = ensure_work(p, d)) return rc;
@@ -723,7 +774,8 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
 
   // ---------------- MobileNetV3-Small body ----------------
   std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
-  HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], st));
+  if (split) HIP_TRY(hipMemsetAsync(w.sc, 0, 2 * sizeof(float), st));
+  HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], split ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
   for (int i = 0; i < 11; ++i) {
@@ -756,26 +808,31 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
 
   // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
   const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
-  const bool split = p->precision == KPD_PRECISION_MIXED && p->fpn0s.hi != nullptr;
   std::unique_ptr<Stage> lat_stage(new Stage(p, "fpn_lateral", st));
   for (int i = 3; i >= 0; --i) {
     const DevConv& L = p->lat[i];
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
-    if (i == 0 && split) HIP_TRY(hipMemsetAsync(w.amax, 0, sizeof(float), st));
+    if (i == 0 && L.cin_p <= 32) {   // the 16-channel stem tap: a 403 MB/step stream, not a GEMM
+      HIP_TRY(launch_lateral_stream(taps[0], L.cin_p, (const float*)L.w, L.b, res, B, lh[0], lw[0], lh[1], lw[1],
+                                    w.lat[0], nullptr, split ? w.sc : nullptr, p->fpn0s.maxb, p->fpn0s.maxs, st));
+      continue;
+    }
+    if (i == 0 && split) return fail(KPD_EINVAL, "split FPN needs the 16-channel stem tap");
     if (int rc = conv(L, taps[i], B, lh[i], lw[i], pad16(kFpnIn[i]), w.lat[i], ACT_NONE, res,
                       i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st,
-                      (i == 0 && split) ? w.amax : nullptr))
+                      (i == 1 && split) ? w.sc + 1 : nullptr))
       return rc;
   }
   lat_stage.reset();
   std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
   if (split) {
-    Split16Args sa{};
-    sa.in = w.lat[0]; sa.w_hi = p->fpn0s.hi; sa.w_lo = p->fpn0s.lo; sa.bias = p->fpn0.b; sa.out = w.feat;
-    sa.stats = d.fused_stats ? w.stats : nullptr; sa.amax = w.amax;
-    sa.N = B; sa.H = d.Hf; sa.W = d.Wf; sa.cin = 128; sa.cout_p = 128; sa.act = ACT_RELU; sa.M = B * HWf;
-    sa.tiles_per_img = d.tiles; sa.w_exp = p->fpn0s.w_exp;
-    HIP_TRY(launch_conv3x3_split16(sa, st));
+    Conv16Args a{};
+    a.in = w.lat[0]; a.wt = p->fpn0s.hl; a.bias = p->fpn0.b; a.out = w.feat;
+    a.stats = d.fused_stats ? w.stats : nullptr;
+    a.N = B; a.H = d.Hf; a.W = d.Wf; a.cin_e = 256; a.cout_p = 128; a.in_cstride = 256; a.out_cstride = 128;
+    a.act = ACT_RELU; a.M = B * HWf; a.tiles_per_img = d.tiles;
+    a.sc_in = w.sc; a.sc_maxb = p->fpn0s.maxb; a.sc_maxs = p->fpn0s.maxs; a.w_exp = p->fpn0s.w_exp;
+    HIP_TRY(launch_conv16(a, 1, 0, st));
   } else if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
                            d.fused_stats ? w.stats : nullptr, d.tiles, 0, st)) {
     return rc;
@@ -828,18 +885,13 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, bf ? 1 : 0, st));
   att_stage.reset();
   std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
-  if (int rc = conv(p->hm1, w.xs, R, 56, 56, 64, w.h1, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 1, st))
-    return rc;
+  if (int rc = hm_conv(p->hm1, w.xs, R, 64, w.h1, 1, st)) return rc;
   c1.reset();
   std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
-  if (int rc = conv(p->hm2, w.h1, R, 56, 56, p->hm1.cout_p, w.h2, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 1,
-                    st))
-    return rc;
+  if (int rc = hm_conv(p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st)) return rc;
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
-  if (int rc = conv(p->hm3, w.h2, R, 56, 56, p->hm2.cout_p, w.h3, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 2,
-                    st))
-    return rc;
+  if (int rc = hm_conv(p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st)) return rc;
   c3.reset();
   {
     Stage sg(p, "hm_final_decode", st);

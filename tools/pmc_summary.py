@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh) per kernel.
 
-HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
-(MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a
-wide 16-B/lane coalesced read stream -- every staging load of the conv
-kernels is a 16-B/lane load; WRITE_SIZE is read as-is).  Both counters are
-in KB.  Writes <outdir>/pmc.json and prints a table."""
+Every counter is averaged per dispatch of a kernel.  When FETCH_SIZE and
+WRITE_SIZE are present, HBM bytes per launch = 2 * FETCH_SIZE * 1024 +
+WRITE_SIZE * 1024 (MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half
+the bytes of a wide 16-B/lane coalesced read stream -- the conv staging loads
+are 16-B/lane loads; WRITE_SIZE is read as-is; both in KB).  Derived stall
+ratios are printed when the SQ counters are present.  Writes <outdir>/pmc.json.
+"""
 import csv
 import glob
 import json
@@ -14,44 +16,55 @@ import sys
 from collections import defaultdict
 
 STAGE_OF = {   # kernel-name substring -> "<stage>:<bench precision>"
-    "conv_mfma_kernel<float, float, 3, 128, 128, 32>": "fpn0:fp32",
-    "conv3x3_split16_kernel": "fpn0:mixed",
+    "conv_mfma_kernel<float, float, 3, 128, 128, 32": "fpn0:fp32",
+    "conv16_kernel<true": "fpn0:mixed",
 }
 
 
-def load(pattern):
-    vals = defaultdict(list)
-    for f in glob.glob(pattern, recursive=True):
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                name = row.get("Kernel_Name", "")
-                v = row.get("Counter_Value")
-                if v is None:
-                    continue
-                vals[name].append(float(v))
-    return vals
+def short(name):
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(ConvArgs")[0].split("(Split16")[0]
 
 
 def main(outdir):
-    fetch = load(os.path.join(outdir, "FETCH_SIZE", "**", "*counter_collection.csv"))
-    write = load(os.path.join(outdir, "WRITE_SIZE", "**", "*counter_collection.csv"))
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Value") is None:
+                    continue
+                vals[short(row.get("Kernel_Name", ""))][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {}
-    for name in sorted(set(fetch) | set(write)):
-        f = fetch.get(name, [])
-        w = write.get(name, [])
-        fk = sum(f) / len(f) if f else 0.0
-        wk = sum(w) / len(w) if w else 0.0
-        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(ConvArgs")[0]
-        entry = {"fetch_kb": fk, "write_kb": wk, "launches": max(len(f), len(w)),
-                 "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-        res[short] = entry
-        for k, stage in STAGE_OF.items():
-            if k in short:
-                res[stage] = dict(entry, kernel=short,
-                                  correction="2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 16B/lane reads)")
-    for k, e in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
-        print(f"{e['hbm_bytes_per_launch'] / 1e6:12.2f} MB  fetch {e['fetch_kb'] / 1024:10.1f} MiB  "
-              f"write {e['write_kb'] / 1024:10.1f} MiB  x{e['launches']:4d}  {k[:110]}")
+    for k, cs in vals.items():
+        e = {c: sum(v) / len(v) for c, v in cs.items()}
+        e["launches"] = max(len(v) for v in cs.values())
+        if "FETCH_SIZE" in e or "WRITE_SIZE" in e:
+            e["hbm_bytes_per_launch"] = 2 * e.get("FETCH_SIZE", 0.0) * 1024 + e.get("WRITE_SIZE", 0.0) * 1024
+        wc = e.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                      "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_LDS"):
+                if c in e:
+                    e["frac_" + c] = e[c] / wc
+        if e.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_conflict_ratio"] = e.get("SQ_LDS_BANK_CONFLICT", 0.0) / e["SQ_LDS_IDX_ACTIVE"]
+        res[k] = e
+        for sub, stage in STAGE_OF.items():
+            if sub in k:
+                res[stage] = dict(e, kernel=k, correction="2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 16B/lane reads)")
+    order = sorted(res.items(), key=lambda kv: -kv[1].get("hbm_bytes_per_launch", kv[1].get("SQ_WAVE_CYCLES", 0)))
+    for k, e in order:
+        if ":" in k:
+            continue
+        parts = []
+        if "hbm_bytes_per_launch" in e:
+            parts.append(f"{e['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch")
+        for c in sorted(e):
+            if c.startswith("frac_") or c == "lds_conflict_ratio":
+                parts.append(f"{c.replace('frac_SQ_', '')}={e[c]:.3f}")
+        for c in ("SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+            if c in e:
+                parts.append(f"{c.replace('SQ_', '')}={e[c]:.3g}")
+        print(f"x{e['launches']:4d} {k[:70]:70s} " + " ".join(parts))
     with open(os.path.join(outdir, "pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1)
 
