@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc_fpn0.json"),
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
 
@@ -180,7 +180,9 @@ def main():
     for s in ("hm_conv1", "hm_conv2", "hm_conv3"):
         mfma[s] = (fl[s] * B, PEAK_TFLOPS["bf16" if mixed else "fp32"],
                    f"{s} implicit-GEMM conv3x3 ({'bf16' if mixed else 'fp32'} MFMA)")
-    dom = max(stages, key=lambda k: stages[k]) if stages else None
+    # dominant KERNEL: the longest single-kernel MFMA stage ("body" is ~50 small launches)
+    cand = [s for s in mfma if s in stages]
+    dom = max(cand, key=lambda k: stages[k]) if cand else None
     roof = None
     if dom in mfma:
         flop, peak, desc = mfma[dom]

@@ -47,12 +47,28 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int BM = 256, NT = 512, ROWB = 128;
 constexpr unsigned OOB = 0x80000000u;   // out-of-range voffset: the buffer load returns 0
 
-// one LDS-DMA wave-instruction: 16 bytes per lane from rsrc[voff + soff] to
-// (kept out of the kernel template: hipcc/ROCm 7.2 silently drops the host
-// stub of a template kernel that calls this builtin directly)
-// lds_dst + 16 * lane (lds_dst wave-uniform; out-of-range offsets load zeros)
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rsrc, char* lds_dst, unsigned voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)lds_dst, 16, voff, soff, 0, 0);
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// raw buffer descriptor: base, stride 0, num_records = bytes (range-checked)
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  return i32x4{(int)(unsigned)a, (int)((a >> 32) & 0xffffu), bytes, 0x00020000};
+}
+
+// One LDS-DMA wave-instruction: 16 bytes per lane from rsrc[voff + soff] to
+// LDS byte address lds_dst + 16 * lane (lds_dst wave-uniform; an out-of-range
+// offset loads zeros).  Inline asm on purpose: hipcc does not see these loads,
+// so it neither drains them with vmcnt(0) before the next ds_read nor at a
+// barrier -- the kernel counts them itself (wait_vmcnt).  M0 is written and
+// restored inside the statement (guide §5.7).
+__device__ __forceinline__ void glds16(i32x4 rsrc, unsigned lds_dst, unsigned voff, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_dst), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
 }
 
 template <int N>
@@ -61,7 +77,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool SPLIT, typename TO, int KS, int BN, int S>
+template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF>
 __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
@@ -83,10 +99,11 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   const int H = p.H, W = p.W, HW = H * W, M = p.M;
   const int cin_e = p.cin_e;
 
-  __amdgpu_buffer_rsrc_t rin =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.in), (short)0, p.in_bytes, 0x00020000);
-  __amdgpu_buffer_rsrc_t rwt =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.wt), (short)0, p.wt_bytes, 0x00020000);
+  const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
+  // wave-uniform LDS byte address of this wave's first A / B staging row
+  const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
+  const unsigned a_dst = __builtin_amdgcn_readfirstlane(lds0 + wave * 32 * ROWB);
+  const unsigned b_dst = __builtin_amdgcn_readfirstlane(lds0 + (BM + wave * (BN / 8)) * ROWB);
 
   // LDS-DMA geometry: one wave-instruction fills 8 rows x 128 B; lane l lands
   // in row (l >> 3), physical chunk (l & 7), so it fetches logical chunk
@@ -122,19 +139,20 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   auto issue = [&](int stage) {
     const int dy = ld_tap / KS - KS / 2, dx = ld_tap % KS - KS / 2;
     const int delta = ((dy * W + dx) * p.in_cstride + ld_kc * 64) * 2;
-    char* sbase = lds + stage * STAGE;
+    const unsigned so = stage * STAGE;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const unsigned voff = ((a_taps[i] >> ld_tap) & 1u) ? a_off[i] + delta : OOB;
-      glds16(rin, sbase + (wave * 32 + i * 8) * ROWB, voff, 0);
+      glds16(rin, a_dst + so + i * 8 * ROWB, voff, 0);
     }
     const int soff = (ld_tap * cin_e + ld_kc * 64) * 2;
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i)
-      glds16(rwt, sbase + (BM + wave * (BN / 8) + i * 8) * ROWB, b_off[i], soff);
-    if (++ld_kc == kc_per_tap) {
-      ld_kc = 0;
-      ++ld_tap;
+    for (int i = 0; i < B_LD; ++i) glds16(rwt, b_dst + so + i * 8 * ROWB, b_off[i], soff);
+    // taps inner, channel chunks outer: the 9 shifted reads of one chunk's
+    // halo rows come in 9 consecutive K-tiles and hit the XCD's L2
+    if (++ld_tap == KS * KS) {
+      ld_tap = 0;
+      ++ld_kc;
     }
   };
 
@@ -146,68 +164,111 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 
   const int g = lane >> 4, r16 = lane & 15;
   const int a_row = (wm * WM + r16) * ROWB, b_row = (BM + wn * 64 + r16) * ROWB;
-  auto chunk = [&](int c) { return ((c ^ (r16 & 7)) << 4); };
-  auto compute = [&](int stage) {
+  // A K-tile row is 8 chunks; lane group g reads chunk g (q = 0) and 4 + g
+  // (q = 1): bf16 = k-steps 0 / 1, split = hi / lo of one 32-channel k-step.
+  const int ch0 = ((g ^ (r16 & 7)) << 4), ch1 = (((4 + g) ^ (r16 & 7)) << 4);
+  struct Frag {
+    uint4 a[2][FM], b[2][FN];
+  };
+  auto load_frags = [&](int stage, Frag& f) {
     const char* sb = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      f.a[0][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch0);
+      f.a[1][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch1);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      f.b[0][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch0);
+      f.b[1][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch1);
+    }
+  };
+  auto mma = [&](const Frag& f) {
     if constexpr (SPLIT) {
-      f16x8 ah[FM], al[FM], bh[FN], bl[FN];
-      const int ch = chunk(g), cl = chunk(4 + g);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        ah[i] = *reinterpret_cast<const f16x8*>(sb + a_row + i * 16 * ROWB + ch);
-        al[i] = *reinterpret_cast<const f16x8*>(sb + a_row + i * 16 * ROWB + cl);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        bh[j] = *reinterpret_cast<const f16x8*>(sb + b_row + j * 16 * ROWB + ch);
-        bl[j] = *reinterpret_cast<const f16x8*>(sb + b_row + j * 16 * ROWB + cl);
-      }
+      // three passes over the accumulators so consecutive MFMAs are independent
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
+                                                             __builtin_bit_cast(f16x8, f.b[1][j]), acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[1][i]),
+                                                             __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
+                                                             __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 av[FM], bv[FN];
-        const int c = chunk(ks * 4 + g);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const bf16x8*>(sb + a_row + i * 16 * ROWB + c);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const bf16x8*>(sb + b_row + j * 16 * ROWB + c);
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[q][i]),
+                                                                __builtin_bit_cast(bf16x8, f.b[q][j]), acc[i][j], 0,
+                                                                0, 0);
     }
   };
+  auto tile_ready = [&](int k) {   // every wave's LDS-DMA of tile k landed + all fragment reads done
+    if (k + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
+    else wait_vmcnt<0>();
+    // lgkmcnt(0) as the builtin (vmcnt/expcnt fields at max), so hipcc knows the
+    // fragment registers are complete and adds no waits inside the MFMA block
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
 
-  // ---- S-stage ring: tile k lives in stage k % S ----
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < KT) issue(s);
-  int cs = 0;                 // stage of the tile being computed
-  int is = S - 1;             // stage the next issue writes
-  for (int kt = 0; kt < KT; ++kt) {
-    // tile kt has landed once at most the tiles issued after it are pending
-    if (kt + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();   // tile kt visible to all; stage of tile kt-1 free
-    asm volatile("" ::: "memory");
-    if (kt + S - 1 < KT) issue(is);
-    compute(cs);
-    cs = cs + 1 == S ? 0 : cs + 1;
-    is = is + 1 == S ? 0 : is + 1;
+  if constexpr (PF) {
+    // Fragment prefetch: after barrier k the waves read tile k+1's fragments
+    // while the MFMAs of tile k (already in registers) run, so a barrier never
+    // leaves the MFMA pipe waiting on LDS latency.  Tile k+S-1 goes into the
+    // stage of tile k-1, whose fragments every wave finished reading before
+    // barrier k-1 (lgkmcnt(0) ahead of each barrier).
+    Frag f0, f1;
+    tile_ready(0);
+    load_frags(0, f0);
+    int is = S - 1, rs = 1;   // stage the next issue writes / the next fragment read uses
+    auto step = [&](int kt, Frag& cur, Frag& nxt) {
+      if (kt + S - 1 < KT) issue(is);
+      is = is + 1 == S ? 0 : is + 1;
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // cur's fragments complete on every path
+      if (kt + 1 < KT) {
+        tile_ready(kt + 1);
+        load_frags(rs, nxt);
+        rs = rs + 1 == S ? 0 : rs + 1;
+      }
+      __builtin_amdgcn_s_setprio(1);
+      mma(cur);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    int kt = 0;
+    for (; kt + 1 < KT; kt += 2) {
+      step(kt, f0, f1);
+      step(kt + 1, f1, f0);
+    }
+    if (kt < KT) step(kt, f0, f1);
+  } else {
+    int cs = 0, is = S - 1;
+    for (int kt = 0; kt < KT; ++kt) {
+      tile_ready(kt);   // tile kt visible to all; stage of tile kt-1 free
+      if (kt + S - 1 < KT) issue(is);
+      Frag f;
+      load_frags(cs, f);
+      mma(f);
+      cs = cs + 1 == S ? 0 : cs + 1;
+      is = is + 1 == S ? 0 : is + 1;
+    }
   }
   __syncthreads();   // every wave's last LDS read done before the epilogue reuses LDS
 
@@ -231,7 +292,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
 
-template <bool SPLIT, typename TO, int KS, int BN, int S>
+template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF = (BN <= 128)>
 hipError_t launch(const Conv16Args& a0, hipStream_t st) {
   constexpr long OS = sizeof(TO);
   Conv16Args a = a0;
@@ -250,7 +311,7 @@ hipError_t launch(const Conv16Args& a0, hipStream_t st) {
     a.stats = a0.stats ? a0.stats + (long)n0 * a.tiles_per_img * 2 * a.cout_p : nullptr;
     a.in_bytes = (int)(nb * img_bytes);
     dim3 grid(((a.M + BM - 1) / BM) * (a.cout_p / BN));
-    hipLaunchKernelGGL((conv16_kernel<SPLIT, TO, KS, BN, S>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((conv16_kernel<SPLIT, TO, KS, BN, S, PF>), grid, dim3(NT), 0, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

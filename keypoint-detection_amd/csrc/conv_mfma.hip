@@ -22,7 +22,10 @@
 //     to MFMA s) -- legal because A and B use the same permutation.
 //   * Global->LDS is register-staged and double buffered: the next K-tile is
 //     in flight while MFMAs run on the current one; one barrier per K-tile.
-//   * Zero padding of the 3x3 halo is done by predicating the A-tile loads.
+//     K order: channel chunks outer, taps inner (L2 reuse of the halo rows).
+//   * Global loads are buffer loads with 32-bit per-lane offsets fixed over
+//     K; the 3x3 halo and the M tail are zero-filled by the buffer
+//     descriptor's range check (no predicated loads, no branches).
 //   * Epilogue fuses bias (BN folded on the host), activation, residual add
 //     with optional nearest-upsample indexing (FPN top-down), per-image
 //     channel sum/max partials (ChannelAttention pooling), bf16/fp32 stores.
@@ -112,8 +115,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   uint4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
 
   auto load_tile = [&](int kt, uint4 (&ra)[NA], uint4 (&rb)[NB]) {
-    const int tap = kt / kc_per_tap;                       // wave-uniform (SALU)
-    const int ci0 = (kt - tap * kc_per_tap) * BK;
+    // taps inner, channel chunks outer (wave-uniform, SALU): the 9 shifted
+    // reads of one chunk come in consecutive K-tiles and hit L2
+    const int kc = kt / (KS * KS), tap = kt - kc * (KS * KS);
+    const int ci0 = kc * BK;
     const int delta = (((tap / KS - KS / 2) * W + (tap % KS - KS / 2)) * p.in_cstride + ci0) * ES;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
