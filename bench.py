@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-batch streams inside one forward (kpd_plan_set_streams)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
@@ -121,7 +123,7 @@ def main():
     from dll.models import MultiPersonKeypointModel
     from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
 
-    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=a.precision)
+    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=a.precision, streams=a.streams)
     sd = synthetic_state_dict(m.state_dict(), seed=0)
     m.load_state_dict(sd)
     m = m.to(dev).eval()
@@ -172,13 +174,16 @@ def main():
             stages[s] = ms / n
     fl = flops_per_image(a.height, a.width, P)
     mixed = a.precision == "mixed"
+    # every stage record is one sub-batch launch (kpd_forward splits B >= 32 over streams)
+    n_sub = max(1, min(a.streams, 4, B // 16))
+    Bl = B / n_sub
     # (label, peak TFLOP/s for the ALGORITHMIC flops, kernel description)
-    mfma = {"fpn0": (fl["fpn0"] * B, PEAK_TFLOPS["bf16"] / 3.0 if mixed else PEAK_TFLOPS["fp32"],
+    mfma = {"fpn0": (fl["fpn0"] * Bl, PEAK_TFLOPS["bf16"] / 3.0 if mixed else PEAK_TFLOPS["fp32"],
                      "fpn0 conv3x3 128->128: fp32-accurate 3-product f16 split on v_mfma_f32_16x16x32_f16 "
                      "(peak = 2500/3 TF/s fp32-equivalent)" if mixed else
                      "fpn0 conv3x3 128->128 on v_mfma_f32_16x16x4_f32")}
     for s in ("hm_conv1", "hm_conv2", "hm_conv3"):
-        mfma[s] = (fl[s] * B, PEAK_TFLOPS["bf16" if mixed else "fp32"],
+        mfma[s] = (fl[s] * Bl, PEAK_TFLOPS["bf16" if mixed else "fp32"],
                    f"{s} implicit-GEMM conv3x3 ({'bf16' if mixed else 'fp32'} MFMA)")
     # dominant KERNEL: the longest single-kernel MFMA stage ("body" is ~50 small launches)
     cand = [s for s in mfma if s in stages]
@@ -212,7 +217,7 @@ def main():
         "config": {"workload": "C2: batch 64/GPU, 256x192x3, 1 box/img, heatmap head + soft-argmax decode",
                    "model": "MultiPersonKeypointModel (MobileNetV3-Small+FPN, HeatmapHead)",
                    "global_batch": B * world, "height": a.height, "width": a.width, "persons": P,
-                   "precision": a.precision, "parallelism": f"dp{world}",
+                   "precision": a.precision, "parallelism": f"dp{world}", "streams_per_gpu": n_sub,
                    "gather": bool(gather)},
         "gflop_per_image": round(fl["total"] / 1e9, 3),
         "achieved_tflops_total": round(fl["total"] * total_imgs / el / 1e12, 2),

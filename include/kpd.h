@@ -115,6 +115,20 @@ int kpd_plan_timing_query(kpd_plan* plan, const char* stage, double* total_ms, i
 int kpd_nms(const float* boxes, const float* scores, int n, float iou_threshold, int max_output,
             int32_t* keep, int32_t* n_keep, void* stream);
 
+/* Concurrency: a forward pass over B >= 32 images runs as min(n, B/16)
+ * contiguous sub-batches on as many streams (forked from / joined back into
+ * the caller's stream), so the latency-bound small launches of one sub-batch
+ * overlap the other's.  n in [1, 4]; default 2.  Results do not depend on n
+ * beyond fp32 rounding in the mixed-precision FPN scale. */
+int kpd_plan_set_streams(kpd_plan* plan, int n);
+
+/* Diagnostics (not part of the reference interface): times the LDS-DMA 3x3
+ * conv (conv_glds.hip) on synthetic operands, N x H x W pixels, cin -> cout;
+ * split != 0 selects the fp32-accurate FPN level-0 form (cin = cout = 128).
+ * dbg: 0 full kernel, 1 without the K-loop loads, 2 without the MFMAs,
+ * 4 with an L2-resident A working set.  *ms = mean time per launch. */
+int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cout, int dbg, int iters, float* ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
     __syncthreads();
     if (threadIdx.x == 0) {
       const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      if (bm > 0.f) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(bm));
+      amax_publish(amax, bm);
     }
   }
 }
@@ -98,79 +98,92 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ i
   *reinterpret_cast<float4*>(out + pix * Cp + q * 4) = o;
 }
 
-// One workgroup per image.  x: [N][HW][Cp]; w1 = fc1 transposed [C][sq];
-// w2 = fc2 transposed [sq][C] (C and sq are even in MobileNetV3-Small).
-__global__ __launch_bounds__(256) void se_kernel(const float* __restrict__ x, int HW, int C, int Cp,
-                                                 const float* __restrict__ w1, const float* __restrict__ b1,
-                                                 const float* __restrict__ w2, const float* __restrict__ b2,
-                                                 int sq, float* __restrict__ scale) {
-  __shared__ float4 part[256];
-  __shared__ float mean[1024];
+// Squeeze-excitation, one 1024-thread workgroup (16 waves) per image: the
+// three steps are dependent, so each is laid out for memory-level parallelism
+// (all of a step's loads in flight together) rather than per-thread loops.
+//   x: [N][HW][Cp]; w1 = fc1 [sq][C] (row-major, as stored); w2t = fc2
+//   TRANSPOSED [sq][C]; scale out: [N][Cp] (hardsigmoid, 0 in padding).
+// torchvision SqueezeExcitation (backbone.py:250 via mobilenet_v3_small).
+constexpr int kSeThreads = 1024;
+__global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict__ x, int HW, int C, int Cp,
+                                                        const float* __restrict__ w1, const float* __restrict__ b1,
+                                                        const float* __restrict__ w2t, const float* __restrict__ b2,
+                                                        int sq, float* __restrict__ scale) {
+  __shared__ float4 part[kSeThreads];
+  __shared__ __attribute__((aligned(16))) float mean[1024];
   __shared__ float hid[256];
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const int nq = Cp >> 2;                 // <= 256 (host checks Cp <= 1024)
-  const int rows = 256 / nq;              // pixel strides sharing one channel quad
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nq = Cp >> 2;                       // <= 256
+  const int groups = kSeThreads / nq;           // pixel groups sharing a channel quad
   const float* xb = x + (size_t)n * HW * Cp;
+  // (1) pool: thread (q, g) sums pixels g, g + groups, ... -- loads independent
   {
-    const int q = tid % nq, pr = tid / nq;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (pr < rows) {
-      // 4 independent partial sums so four loads are in flight per thread
-      float4 s1 = s, s2 = s, s3 = s;
-      int p = pr;
-      for (; p + 3 * rows < HW; p += 4 * rows) {
-        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)p * Cp + q * 4);
-        const float4 b = *reinterpret_cast<const float4*>(xb + (size_t)(p + rows) * Cp + q * 4);
-        const float4 c = *reinterpret_cast<const float4*>(xb + (size_t)(p + 2 * rows) * Cp + q * 4);
-        const float4 d = *reinterpret_cast<const float4*>(xb + (size_t)(p + 3 * rows) * Cp + q * 4);
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    const int q = tid % nq, g = tid / nq;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    if (g < groups) {
+      int pix = g;
+      for (; pix + groups < HW; pix += 2 * groups) {
+        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
+        const float4 b = *reinterpret_cast<const float4*>(xb + (size_t)(pix + groups) * Cp + q * 4);
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
         s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
-        s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
-        s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
       }
-      for (; p < HW; p += rows) {
-        const float4 v = *reinterpret_cast<const float4*>(xb + (size_t)p * Cp + q * 4);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      if (pix < HW) {
+        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
       }
-      s.x += s1.x + s2.x + s3.x; s.y += s1.y + s2.y + s3.y;
-      s.z += s1.z + s2.z + s3.z; s.w += s1.w + s2.w + s3.w;
+      s0.x += s1.x; s0.y += s1.y; s0.z += s1.z; s0.w += s1.w;
     }
-    part[tid] = s;
+    part[tid] = s0;
   }
   __syncthreads();
   if (tid < nq) {
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = 0; r < rows; ++r) {
-      const float4 v = part[r * nq + tid];
+    for (int g = 0; g < groups; ++g) {
+      const float4 v = part[g * nq + tid];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
     const float hw = (float)HW;
-    mean[tid * 4 + 0] = t.x / hw; mean[tid * 4 + 1] = t.y / hw;
-    mean[tid * 4 + 2] = t.z / hw; mean[tid * 4 + 3] = t.w / hw;
+    *reinterpret_cast<float4*>(mean + tid * 4) = make_float4(t.x / hw, t.y / hw, t.z / hw, t.w / hw);
   }
   __syncthreads();
-  // fc1 / fc2 as GEMVs over host-TRANSPOSED weights (w1t [C][sq], w2t [sq][C]):
-  // thread = output, lanes read consecutive outputs of one weight row, so
-  // every load instruction is one coalesced 256-B row segment and the loop
-  // carries no address dependence (deep load pipelining).
-  for (int j = tid; j < sq; j += 256) {
-    float a0 = 0.f, a1 = 0.f;
-#pragma unroll 8
-    for (int c = 0; c < C; c += 2) {
-      a0 = fmaf(w1[(size_t)c * sq + j], mean[c], a0);
-      a1 = fmaf(w1[(size_t)(c + 1) * sq + j], mean[c + 1], a1);
+  // (2) fc1 + ReLU: wave per output row, lanes split K with 16-byte loads;
+  // up to 3 rows x 4 K-chunks (C <= 1024) issued before the reductions
+  const int nch = (C + 255) / 256;
+  for (int j0 = wave * 3; j0 < sq; j0 += 16 * 3) {
+    float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int j = j0 + r;
+      if (j < sq) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int c = t * 256 + lane * 4;
+          if (t < nch && c < C) {
+            const float4 wv = *reinterpret_cast<const float4*>(w1 + (size_t)j * C + c);
+            const float4 mv = *reinterpret_cast<const float4*>(mean + c);
+            acc[r] = fmaf(wv.x, mv.x, fmaf(wv.y, mv.y, fmaf(wv.z, mv.z, fmaf(wv.w, mv.w, acc[r]))));
+          }
+        }
+      }
     }
-    hid[j] = fmaxf(a0 + a1 + b1[j], 0.f);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const float v = wave_sum(acc[r]);
+      if (lane == 0 && j0 + r < sq) hid[j0 + r] = fmaxf(v + b1[j0 + r], 0.f);
+    }
   }
   __syncthreads();
-  for (int c = tid; c < Cp; c += 256) {
+  // (3) fc2 + hardsigmoid: thread per output over the transposed weights
+  // (coalesced rows), K unrolled 8-deep with two accumulators
+  for (int c = tid; c < Cp; c += kSeThreads) {
     float v = 0.f;
     if (c < C) {
       float a0 = 0.f, a1 = 0.f;
 #pragma unroll 8
       for (int j = 0; j < sq; j += 2) {
-        a0 = fmaf(w2[(size_t)j * C + c], hid[j], a0);
-        a1 = fmaf(w2[(size_t)(j + 1) * C + c], hid[j + 1], a1);
+        a0 = fmaf(w2t[(size_t)j * C + c], hid[j], a0);
+        a1 = fmaf(w2t[(size_t)(j + 1) * C + c], hid[j + 1], a1);
       }
       v = kpd_hsigmoid(a0 + a1 + b2[c]);
     }
@@ -251,7 +264,7 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
     __syncthreads();
     if (tid == 0) {
       const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      if (bm > 0.f) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(bm));
+      amax_publish(amax, bm);
     }
   }
 }
@@ -300,8 +313,8 @@ hipError_t launch_dwconv(const float* in, const float* w, const float* b, float*
 
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st) {
-  if (Cp > 1024 || sq > 256 || C % 4 || sq % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(se_kernel, dim3(N), dim3(256), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale);
+  if (Cp > 1024 || sq > 256 || C % 4 || sq % 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(se_kernel, dim3(N), dim3(kSeThreads), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale);
   return hipGetLastError();
 }
 

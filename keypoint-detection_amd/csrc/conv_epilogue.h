@@ -11,7 +11,7 @@ struct EpiArgs {
   void* out;           // NHWC rows of out_cstride elements
   const float* res;    // optional residual NHWC [N][rh][rw][cout_p] (nearest-upsampled when rh != H)
   float* stats;        // optional [N][tiles_per_img][2][cout_p] (requires HW % BM == 0)
-  float* amax;         // optional atomicMax of |out|
+  float* amax;         // optional max|out| (slotted, amax_publish)
   float scale;         // acc multiplier before bias (split16 unscale), 1 otherwise
   int M, H, W, cout_p, out_cstride, rh, rw, act, tiles_per_img;
   // optional second per-channel affine after the activation (an un-foldable BN
@@ -77,49 +77,70 @@ __device__ __forceinline__ void store4<__bf16>(__bf16* dst, const float4& v) {
 
 // Requires a __syncthreads() between acc_to_lds and this call (done inside).
 // NT = threads of the workgroup; LDS behind the tile holds 2*NT stats floats.
+// Two passes over a fixed per-thread set of (row, 4-column) cells: every
+// global load (bias, second affine, residual) is issued before the first
+// store -- hipcc cannot prove `out` does not alias them, so interleaving loads
+// and stores would serialise one memory round trip per cell.
 template <typename TO, int BM, int BN, int NT = 256>
 __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0, int n0) {
   constexpr int P = BN + 4, C4 = BN / 4;
+  static_assert(NT % C4 == 0 && (BM * C4) % NT == 0, "epilogue layout");
+  constexpr int RS = NT / C4, IT = BM / RS;   // rows per pass, cells per thread
   const int tid = threadIdx.x;
+  const int c4 = tid % C4, row0 = tid / C4;
+  const int co = n0 + c4 * 4;
+  const bool col_ok = co < p.cout_p;
   __syncthreads();
   float amax = 0.f;
   TO* out = reinterpret_cast<TO*>(p.out);
   const int HW = p.H * p.W;
-  for (int idx = tid; idx < BM * C4; idx += NT) {
-    const int row = idx / C4, c4 = idx - row * C4;
-    const int m = m0 + row, co = n0 + c4 * 4;
-    if (m >= p.M || co >= p.cout_p) continue;
-    float4 v = *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
-    const float4 b = *reinterpret_cast<const float4*>(p.bias + co);
-    v.x = kpd_act(v.x * p.scale + b.x, p.act);
-    v.y = kpd_act(v.y * p.scale + b.y, p.act);
-    v.z = kpd_act(v.z * p.scale + b.z, p.act);
-    v.w = kpd_act(v.w * p.scale + b.w, p.act);
+  float4 b = make_float4(0.f, 0.f, 0.f, 0.f), ps = b, pt = b;
+  if (col_ok) {
+    b = *reinterpret_cast<const float4*>(p.bias + co);
     if (p.post_scale) {
-      const float4 s = *reinterpret_cast<const float4*>(p.post_scale + co);
-      const float4 t = *reinterpret_cast<const float4*>(p.post_shift + co);
-      v.x = kpd_act(v.x * s.x + t.x, p.act2); v.y = kpd_act(v.y * s.y + t.y, p.act2);
-      v.z = kpd_act(v.z * s.z + t.z, p.act2); v.w = kpd_act(v.w * s.w + t.w, p.act2);
+      ps = *reinterpret_cast<const float4*>(p.post_scale + co);
+      pt = *reinterpret_cast<const float4*>(p.post_shift + co);
     }
-    if (p.res) {
-      const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
-      int sy = y, sx = x;
+  }
+  float4 v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int row = row0 + it * RS, m = m0 + row;
+    float4 x = *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
+    x.x = kpd_act(x.x * p.scale + b.x, p.act);
+    x.y = kpd_act(x.y * p.scale + b.y, p.act);
+    x.z = kpd_act(x.z * p.scale + b.z, p.act);
+    x.w = kpd_act(x.w * p.scale + b.w, p.act);
+    if (p.post_scale) {
+      x.x = kpd_act(x.x * ps.x + pt.x, p.act2); x.y = kpd_act(x.y * ps.y + pt.y, p.act2);
+      x.z = kpd_act(x.z * ps.z + pt.z, p.act2); x.w = kpd_act(x.w * ps.w + pt.w, p.act2);
+    }
+    if (p.res && col_ok && m < p.M) {
+      const int n = m / HW, r = m - n * HW, y = r / p.W, xx = r - y * p.W;
+      int sy = y, sx = xx;
       if (p.rh != p.H) sy = min((int)floorf((float)y * ((float)p.rh / (float)p.H)), p.rh - 1);
-      if (p.rw != p.W) sx = min((int)floorf((float)x * ((float)p.rw / (float)p.W)), p.rw - 1);
+      if (p.rw != p.W) sx = min((int)floorf((float)xx * ((float)p.rw / (float)p.W)), p.rw - 1);
       const float4 q = *reinterpret_cast<const float4*>(p.res + ((size_t)(n * p.rh + sy) * p.rw + sx) * p.cout_p + co);
-      v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+      x.x += q.x; x.y += q.y; x.z += q.z; x.w += q.w;
     }
     if (p.act3) {
-      v.x = kpd_act(v.x, p.act3); v.y = kpd_act(v.y, p.act3);
-      v.z = kpd_act(v.z, p.act3); v.w = kpd_act(v.w, p.act3);
+      x.x = kpd_act(x.x, p.act3); x.y = kpd_act(x.y, p.act3);
+      x.z = kpd_act(x.z, p.act3); x.w = kpd_act(x.w, p.act3);
     }
-    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    store4<TO>(out + (size_t)m * p.out_cstride + co, v);
-    if (p.stats) *reinterpret_cast<float4*>(tile + row * P + c4 * 4) = v;
+    v[it] = x;
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int row = row0 + it * RS, m = m0 + row;
+    if (m >= p.M || !col_ok) continue;
+    const float4 x = v[it];
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    store4<TO>(out + (size_t)m * p.out_cstride + co, x);
+    if (p.stats) *reinterpret_cast<float4*>(tile + row * P + c4 * 4) = x;
   }
   if (p.amax) {
     const float w = wave_max(amax);
-    if ((tid & 63) == 0 && w > 0.f) atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(w));
+    if ((tid & 63) == 0) amax_publish(p.amax, w);
   }
   if (p.stats) {
     // column sums / maxima: NT/BN row groups in parallel, then one combine

@@ -77,7 +77,9 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF>
+// DBG (kpd_bench_conv16 only): 1 = no LDS-DMA in the K loop, 2 = no MFMA,
+// 4 = every block reads the same 256 A rows (L2-resident working set)
+template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF, int DBG = 0>
 __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
@@ -117,7 +119,8 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
     a_taps[i] = 0;
     if (m < M) {
       const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
-      a_off[i] = (unsigned)(m * p.in_cstride * 2 + lchunk * 16);
+      const int ms = (DBG & 4) ? (m % BM) + W + 1 : m;
+      a_off[i] = (unsigned)(ms * p.in_cstride * 2 + lchunk * 16);
 #pragma unroll
       for (int t = 0; t < KS * KS; ++t) {
         const int yy = y + t / KS - KS / 2, xx = x + t % KS - KS / 2;
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   // loader state (wave-uniform): next K-tile to issue as (tap, kc)
   int ld_tap = 0, ld_kc = 0;
   auto issue = [&](int stage) {
+    if constexpr ((DBG & 1) != 0) return;
     const int dy = ld_tap / KS - KS / 2, dx = ld_tap % KS - KS / 2;
     const int delta = ((dy * W + dx) * p.in_cstride + ld_kc * 64) * 2;
     const unsigned so = stage * STAGE;
@@ -184,6 +188,10 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
     }
   };
   auto mma = [&](const Frag& f) {
+    if constexpr ((DBG & 2) != 0) {
+      acc[0][0][0] += __uint_as_float(f.a[0][0].x ^ f.b[1][FN - 1].w);   // keep the fragment reads alive
+      return;
+    }
     if constexpr (SPLIT) {
       // three passes over the accumulators so consecutive MFMAs are independent
 #pragma unroll
@@ -337,4 +345,63 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
   if (a.cout_p % 64 == 0)
     return out_bf16 ? launch<false, __bf16, 3, 64, 3>(a, st) : launch<false, float, 3, 64, 3>(a, st);
   return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------- diagnostics
+// Times conv16 variants on synthetic operands (DESIGN.md "K6b" measurements):
+// split != 0 -> the FPN level-0 configuration (cin 128 as hi|lo, cout 128),
+// else bf16 cin -> cout.  dbg selects the ablation (see DBG above).
+template <int DBG>
+static hipError_t bench_launch(const Conv16Args& a, int split, hipStream_t st) {
+  dim3 grid(((a.M + BM - 1) / BM) * (a.cout_p / 128));
+  if (split) hipLaunchKernelGGL((conv16_kernel<true, float, 3, 128, 3, true, DBG>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv16_kernel<false, __bf16, 3, 128, 3, true, DBG>), grid, dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cout, int dbg, int iters, float* ms) {
+  if (N <= 0 || H <= 0 || W <= 0 || cin % 64 || cout % 128 || iters <= 0 || !ms) return -1;
+  if (split && (cin != 128 || cout != 128)) return -1;
+  Conv16Args a{};
+  const long M = (long)N * H * W;
+  const int cin_e = split ? 2 * cin : cin;
+  const long in_b = M * cin_e * 2, w_b = (long)cout * 9 * cin_e * 2, out_b = M * cout * 4;
+  if (in_b > kMaxDesc) return -1;
+  void *in = nullptr, *wt = nullptr, *out = nullptr, *bias = nullptr, *sc = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = -2;
+  if (hipMalloc(&in, in_b) != hipSuccess || hipMalloc(&wt, w_b) != hipSuccess || hipMalloc(&out, out_b) != hipSuccess ||
+      hipMalloc(&bias, cout * 4) != hipSuccess || hipMalloc(&sc, 2 * kAmaxSlots * kAmaxStride * 4) != hipSuccess)
+    goto done;
+  (void)hipMemset(in, 0x3C, in_b);
+  (void)hipMemset(wt, 0x3A, w_b);
+  (void)hipMemset(bias, 0, cout * 4);
+  (void)hipMemset(sc, 0, 2 * kAmaxSlots * kAmaxStride * 4);
+  a.in = in; a.wt = wt; a.bias = (const float*)bias; a.out = out; a.N = N; a.H = H; a.W = W; a.cin_e = cin_e;
+  a.cout_p = cout; a.in_cstride = cin_e; a.out_cstride = cout; a.act = ACT_RELU; a.M = (int)M;
+  a.sc_in = (const float*)sc; a.sc_maxb = 1.f; a.sc_maxs = 1.f;
+  a.in_bytes = (int)in_b; a.wt_bytes = (int)w_b;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) goto done;
+  for (int it = -2; it < iters; ++it) {
+    if (it == 0) (void)hipEventRecord(e0, 0);
+    hipError_t e = hipSuccess;
+    switch (dbg) {
+      case 0: e = bench_launch<0>(a, split, 0); break;
+      case 1: e = bench_launch<1>(a, split, 0); break;
+      case 2: e = bench_launch<2>(a, split, 0); break;
+      case 4: e = bench_launch<4>(a, split, 0); break;
+      default: e = hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) goto done;
+  }
+  (void)hipEventRecord(e1, 0);
+  if (hipEventSynchronize(e1) != hipSuccess) goto done;
+  (void)hipEventElapsedTime(ms, e0, e1);
+  *ms /= iters;
+  rc = 0;
+done:
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(in); (void)hipFree(wt); (void)hipFree(out); (void)hipFree(bias); (void)hipFree(sc);
+  return rc;
 }

@@ -110,11 +110,15 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   }
 
   const int kc_per_tap = cin_p / BK;
-  const int KT = KS * KS * kc_per_tap;
+  // split-K (blockIdx.y = slice): this block runs K-tiles [kt0, kt0 + KT)
+  const int KT_all = KS * KS * kc_per_tap, ks = blockIdx.y;
+  const int kt0 = (int)((long)KT_all * ks / p.k_split);
+  const int KT = (int)((long)KT_all * (ks + 1) / p.k_split) - kt0;
   // two register stage sets: with PF2 tile k+2 is in flight while tile k is computed
   uint4 ra0[NA], rb0[NB], ra1[NA], rb1[NB];
 
-  auto load_tile = [&](int kt, uint4 (&ra)[NA], uint4 (&rb)[NB]) {
+  auto load_tile = [&](int kk, uint4 (&ra)[NA], uint4 (&rb)[NB]) {
+    const int kt = kt0 + kk;
     // taps inner, channel chunks outer (wave-uniform, SALU): the 9 shifted
     // reads of one chunk come in consecutive K-tiles and hit L2
     const int kc = kt / (KS * KS), tap = kt - kc * (KS * KS);
@@ -229,12 +233,69 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   // ---------------- epilogue (LDS-staged, 16-byte row stores) ----------------
   float* tile = reinterpret_cast<float*>(lds);
   acc_to_lds<FM, FN, WM, WN, BN>(tile, acc, wm, wn, lane);
+  if (p.k_split > 1) {   // raw partial sums; splitk_reduce_kernel applies the epilogue
+    constexpr int P = BN + 4, C4 = BN / 4;
+    __syncthreads();
+    float* dst = p.splitk_ws + (size_t)ks * M * cout_p;
+    for (int idx = tid; idx < BM * C4; idx += 256) {
+      const int row = idx / C4, c4 = idx - row * C4, m = m0 + row, co = n0 + c4 * 4;
+      if (m < M && co < cout_p)
+        *reinterpret_cast<float4*>(dst + (size_t)m * cout_p + co) =
+            *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
+    }
+    return;
+  }
   EpiArgs e;
   e.bias = p.bias; e.out = p.out; e.res = p.res; e.stats = p.stats; e.amax = p.amax; e.scale = 1.f;
   e.M = M; e.H = H; e.W = W; e.cout_p = cout_p; e.out_cstride = p.out_cstride; e.rh = p.rh; e.rw = p.rw;
   e.act = p.act; e.tiles_per_img = p.tiles_per_img;
   e.post_scale = p.post_scale; e.post_shift = p.post_shift; e.act2 = p.act2; e.act3 = p.act3;
   tile_store<TO, BM, BN>(tile, e, m0, n0);
+}
+
+// Split-K reduction + the conv epilogue (bias, act, second affine, residual
+// with nearest upsample, act3, amax) -- partial slices summed in fixed order,
+// so results do not depend on scheduling.  One thread per 4 output channels.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
+  const int C4 = p.cout_p / 4;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  float amax = 0.f;
+  if (idx < (long)p.M * C4) {
+    const int m = (int)(idx / C4), co = (int)(idx - (long)m * C4) * 4;
+    const size_t slice = (size_t)p.M * p.cout_p, off = (size_t)m * p.cout_p + co;
+    float4 x = *reinterpret_cast<const float4*>(p.splitk_ws + off);
+    for (int k = 1; k < p.k_split; ++k) {
+      const float4 q = *reinterpret_cast<const float4*>(p.splitk_ws + k * slice + off);
+      x.x += q.x; x.y += q.y; x.z += q.z; x.w += q.w;
+    }
+    const float4 b = *reinterpret_cast<const float4*>(p.bias + co);
+    x.x = kpd_act(x.x + b.x, p.act); x.y = kpd_act(x.y + b.y, p.act);
+    x.z = kpd_act(x.z + b.z, p.act); x.w = kpd_act(x.w + b.w, p.act);
+    if (p.post_scale) {
+      const float4 s = *reinterpret_cast<const float4*>(p.post_scale + co);
+      const float4 t = *reinterpret_cast<const float4*>(p.post_shift + co);
+      x.x = kpd_act(x.x * s.x + t.x, p.act2); x.y = kpd_act(x.y * s.y + t.y, p.act2);
+      x.z = kpd_act(x.z * s.z + t.z, p.act2); x.w = kpd_act(x.w * s.w + t.w, p.act2);
+    }
+    if (p.res) {
+      const int HW = p.H * p.W, n = m / HW, r = m - n * HW, y = r / p.W, xx = r - y * p.W;
+      int sy = y, sx = xx;
+      if (p.rh != p.H) sy = min((int)floorf((float)y * ((float)p.rh / (float)p.H)), p.rh - 1);
+      if (p.rw != p.W) sx = min((int)floorf((float)xx * ((float)p.rw / (float)p.W)), p.rw - 1);
+      const float4 q = *reinterpret_cast<const float4*>(p.res + ((size_t)(n * p.rh + sy) * p.rw + sx) * p.cout_p + co);
+      x.x += q.x; x.y += q.y; x.z += q.z; x.w += q.w;
+    }
+    if (p.act3) {
+      x.x = kpd_act(x.x, p.act3); x.y = kpd_act(x.y, p.act3);
+      x.z = kpd_act(x.z, p.act3); x.w = kpd_act(x.w, p.act3);
+    }
+    amax = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+    *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)m * p.out_cstride + co) = x;
+  }
+  if (p.amax) {
+    const float w = wave_max(amax);
+    if ((threadIdx.x & 63) == 0) amax_publish(p.amax, w);
+  }
 }
 
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
@@ -247,9 +308,22 @@ hipError_t launch(const ConvArgs& a0, hipStream_t st) {
   const long img_bytes = (long)a.H * a.W * a.in_cstride * ES;
   if (wt_bytes > kMaxDesc || img_bytes > kMaxDesc) return hipErrorInvalidValue;
   a.wt_bytes = (int)wt_bytes;
-  // images per launch so the input descriptor stays below 2^31 bytes
-  const int chunk = (int)std::min<long>(a.N, kMaxDesc / img_bytes);
   const long HW = (long)a.H * a.W;
+  // split-K: a 1x1 fp32 GEMM on a coarse map (MobileNet projects at <= 16x12,
+  // FPN lateral 3) has few output tiles and a long K -- one serial K loop per
+  // block.  Slice K over blockIdx.y and reduce in fixed order.  The slice count
+  // depends on the layer only (never on the batch), so an image's result does
+  // not depend on what it is batched with.
+  const int KT_all = KS * KS * (a.cin_p / BK);
+  a.k_split = 1;
+  if (KS == 1 && sizeof(TA) == 4 && sizeof(TO) == 4 && a.splitk_ws && !a.stats && HW <= 256 && KT_all >= 4 &&
+      a.out_cstride == a.cout_p)
+    a.k_split = std::min(KT_all / 2, 8);
+  // images per launch: input descriptor below 2^31 bytes, partials within the scratch
+  long chunk_l = std::min<long>(a.N, kMaxDesc / img_bytes);
+  if (a.k_split > 1) chunk_l = std::min<long>(chunk_l, a.splitk_cap / (HW * a.cout_p * a.k_split));
+  if (chunk_l < 1) a.k_split = 1, chunk_l = std::min<long>(a.N, kMaxDesc / img_bytes);
+  const int chunk = (int)chunk_l;
   for (int n0 = 0; n0 < a0.N; n0 += chunk) {
     const int nb = std::min(chunk, a0.N - n0);
     a.N = nb;
@@ -260,10 +334,17 @@ hipError_t launch(const ConvArgs& a0, hipStream_t st) {
     a.a_scale = a0.a_scale ? a0.a_scale + (long)n0 * a.cin_p : nullptr;
     a.stats = a0.stats ? a0.stats + (long)n0 * a.tiles_per_img * 2 * a.cout_p : nullptr;
     a.in_bytes = (int)(nb * img_bytes);
-    dim3 grid(((a.M + BM - 1) / BM) * ((a.cout_p + BN - 1) / BN));
+    const int blocks = ((a.M + BM - 1) / BM) * ((a.cout_p + BN - 1) / BN);
+    dim3 grid(blocks, a.k_split);
     hipLaunchKernelGGL((conv_mfma_kernel<TA, TO, KS, BM, BN, BK, PF2>), grid, dim3(256), 0, st, a);
-    const hipError_t e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (a.k_split > 1) {
+      const long n4 = (long)a.M * (a.cout_p / 4);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
   }
   return hipSuccess;
 }

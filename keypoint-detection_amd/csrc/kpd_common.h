@@ -36,13 +36,30 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Device max|x| published by many workgroups: one float per 128-byte slot,
+// kAmaxSlots slots (workgroup b uses slot b % kAmaxSlots), so the atomics of a
+// whole grid spread over L2 channels instead of queueing on one address.
+// Readers take the max over the slots.  The caller zeroes the slots.
+constexpr int kAmaxSlots = 64, kAmaxStride = 32;
+__device__ __forceinline__ void amax_publish(float* slots, float v) {
+  if (v > 0.f)
+    atomicMax(reinterpret_cast<unsigned int*>(slots + (blockIdx.x % kAmaxSlots) * kAmaxStride), __float_as_uint(v));
+}
+// whole-wave call (all 64 lanes): returns the max over the slots in every lane
+__device__ __forceinline__ float amax_read(const float* slots) {
+  return wave_max(slots[(threadIdx.x & 63) * kAmaxStride]);
+}
+
 // Split (fp32-accurate f16 hi+lo) FPN level 0: power-of-two activation
 // exponent from the device-side bound U >= max|lateral0| (producer and
 // consumer evaluate the same expression on the same inputs, so they agree):
 // U = (maxb + max|tap0| * maxs + max|lateral1|) * (1 + 2^-7), a_exp = 14 - e
 // with U < 2^e, hence max|x * 2^a_exp| < 2^14 and the f16 hi part is finite.
+// sc_in = two slotted maxima (amax_publish): [max|tap0|], [max|lateral1|].
+// Whole-wave call.
 __device__ __forceinline__ int split_a_exp(const float* sc_in, float maxb, float maxs) {
-  const float u = (maxb + sc_in[0] * maxs + sc_in[1]) * 1.0078125f;
+  const float a0 = amax_read(sc_in), l1 = amax_read(sc_in + kAmaxSlots * kAmaxStride);
+  const float u = (maxb + a0 * maxs + l1) * 1.0078125f;
   if (!(u > 0.f) || !(u < INFINITY)) return 0;
   int e;
   frexpf(u, &e);

@@ -18,11 +18,16 @@ struct ConvArgs {
   int act;
   int M;                 // N*H*W
   int tiles_per_img;
-  float* amax;           // optional: atomicMax of |out| (float bits; caller zeroes it)
+  float* amax;           // optional: max|out| into kAmaxSlots slots (amax_publish; caller zeroes them)
   const float* post_scale;  // optional second affine after act (see conv_epilogue.h)
   const float* post_shift;
   int act2, act3;
   int in_bytes, wt_bytes;   // buffer-descriptor extents; filled by launch_conv (each < 2^31)
+  // optional split-K scratch for small-M 1x1 fp32 GEMMs (launch_conv decides):
+  // partial sums [k_split][M][cout_p] + a reduce/epilogue kernel, fixed order
+  float* splitk_ws;
+  long splitk_cap;          // floats available at splitk_ws
+  int k_split;              // set by launch_conv
 };
 
 // 16-bit-operand 3x3 conv with LDS-DMA staging (conv_glds.hip): bf16 operands,

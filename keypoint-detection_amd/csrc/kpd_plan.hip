@@ -107,7 +107,8 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   void* h2 = nullptr;
   float* h3 = nullptr;
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
-  float* sc = nullptr;    // split FPN scale inputs: [max|tap0|, max|lateral1|]
+  float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
+  float* sc = nullptr;    // split FPN scale inputs: slotted max|tap0|, max|lateral1| (amax_publish)
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
   float* pd_head = nullptr;     // [B][56*56][48]
@@ -169,12 +170,16 @@ struct kpd_plan {
   float *kh_bn1a_s = nullptr, *kh_bn1a_t = nullptr, *kh_bn1b_s = nullptr, *kh_bn1b_t = nullptr;
   float *kh_lnr_g = nullptr, *kh_lnr_b = nullptr, *kh_fr_w = nullptr, *kh_fr_b = nullptr;
   float *kh_lnv_g = nullptr, *kh_lnv_b = nullptr, *kh_fv_w = nullptr, *kh_fv_b = nullptr;
-  // workspace
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  Dims dims;
-  Work work;
-  bool have_work = false;
+  // workspace, one per concurrent sub-batch (kpd_plan_set_streams)
+  static constexpr int kMaxSub = 4;
+  void* ws[kMaxSub] = {};
+  size_t ws_bytes[kMaxSub] = {};
+  Dims dims[kMaxSub];
+  Work work[kMaxSub];
+  bool have_work[kMaxSub] = {};
+  int streams = 2;                        // requested sub-batch streams
+  hipStream_t sub_st[kMaxSub] = {};       // [0] unused: sub-batch 0 runs on the caller's stream
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::map<std::string, std::pair<const void*, size_t>> debug;
   // per-stage HIP-event timing (kpd_plan_timing)
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; size_t used = 0; };
@@ -365,6 +370,8 @@ int pack_split16(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
 }
 
 // ------------------------------------------------------------------ workspace
+constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
+
 struct Carver {
   char* base;
   size_t off = 0;
@@ -395,7 +402,8 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   for (int i = 0; i < 4; ++i) w.lat[i] = c.take<float>((size_t)B * lh[i] * lw[i] * 128);
   w.feat = c.take<float>((size_t)B * d.Hf * d.Wf * 128);
   w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
-  w.sc = c.take<float>(2);
+  w.sc = c.take<float>(2 * kAmaxSlots * kAmaxStride);
+  w.splitk = c.take<float>(kSplitKFloats);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
@@ -440,6 +448,9 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   return c.off + 256;
 }
 
+// split-K scratch of the workspace the current forward_one uses (set on entry)
+thread_local float* g_splitk = nullptr;
+
 // conv with the second affine + residual + final activation epilogue
 int conv_post(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, void* out, int act,
               const float* ps, const float* pt, int act2, const float* res, int act3, hipStream_t st) {
@@ -449,6 +460,7 @@ int conv_post(const DevConv& L, const void* in, int N, int H, int W, int in_cstr
   a.in_cstride = in_cstride; a.out_cstride = L.cout_p;
   a.rh = H; a.rw = W; a.act = act; a.M = N * H * W;
   a.post_scale = ps; a.post_shift = pt; a.act2 = act2; a.act3 = act3;
+  a.splitk_ws = g_splitk; a.splitk_cap = kSplitKFloats;
   HIP_TRY(launch_conv(a, CONV_F32, L.k, st));
   return KPD_OK;
 }
@@ -485,6 +497,7 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
   a.N = N; a.H = H; a.W = W; a.cin_p = L.cin_p; a.cout_p = L.cout_p;
   a.in_cstride = in_cstride; a.out_cstride = L.cout_p;
   a.rh = rh; a.rw = rw; a.act = act; a.M = N * H * W; a.tiles_per_img = tiles;
+  a.splitk_ws = g_splitk; a.splitk_cap = kSplitKFloats;
   const ConvDType dt = !L.bf16 ? CONV_F32 : (out_kind == 1 ? CONV_BF16_OUT_BF16 : CONV_BF16_OUT_F32);
   HIP_TRY(launch_conv(a, dt, L.k, st));
   return KPD_OK;
@@ -541,7 +554,12 @@ void kpd_plan_destroy(kpd_plan* p) {
   int cur = 0;
   if (hipGetDevice(&cur) == hipSuccess) (void)hipSetDevice(p->device);
   for (void* a : p->allocs) (void)hipFree(a);
-  if (p->ws) (void)hipFree(p->ws);
+  for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
+    if (p->ws[k]) (void)hipFree(p->ws[k]);
+    if (p->sub_st[k]) (void)hipStreamDestroy(p->sub_st[k]);
+    if (p->join_ev[k]) (void)hipEventDestroy(p->join_ev[k]);
+  }
+  if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
   for (auto& kv : p->timers)
     for (auto& e : kv.second.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   (void)hipSetDevice(cur);
@@ -561,8 +579,10 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   p->kh_ds1 = DevConv();
   p->kh_ds2 = DevConv();
   p->has_kh = false;
-  if (p->ws) { (void)hipFree(p->ws); p->ws = nullptr; p->ws_bytes = 0; }
-  p->have_work = false;
+  for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
+    if (p->ws[k]) { (void)hipFree(p->ws[k]); p->ws[k] = nullptr; p->ws_bytes[k] = 0; }
+    p->have_work[k] = false;
+  }
   p->precision = precision;
   std::string missing;
   int rc = KPD_OK;
@@ -605,7 +625,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     if (bn.cfg.se) {
       const std::string s = pre + std::to_string(j);
       bn.se.C = bn.cfg.exp; bn.se.Cp = pad16(bn.cfg.exp); bn.se.sq = se_squeeze(bn.cfg.exp);
-      chk(pack_transposed(p, s + ".fc1.weight", bn.se.sq, bn.se.C, &bn.se.w1, missing));
+      chk(pack_plain(p, s + ".fc1.weight", &bn.se.w1, missing, (size_t)bn.se.sq * bn.se.C));
       chk(pack_plain(p, s + ".fc1.bias", &bn.se.b1, missing, bn.se.sq));
       chk(pack_transposed(p, s + ".fc2.weight", bn.se.C, bn.se.sq, &bn.se.w2, missing));
       chk(pack_plain(p, s + ".fc2.bias", &bn.se.b2, missing, bn.se.C));
@@ -721,40 +741,29 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   return KPD_OK;
 }
 
-static int ensure_work(kpd_plan* p, const Dims& d) {
-  if (p->have_work && p->dims == d) return KPD_OK;
+static int ensure_work(kpd_plan* p, const Dims& d, int k) {
+  if (p->have_work[k] && p->dims[k] == d) return KPD_OK;
   Work w;
   const size_t need = carve(p, d, nullptr, w);
-  if (need > p->ws_bytes) {
-    if (p->ws) HIP_TRY(hipFree(p->ws));
-    p->ws = nullptr;
-    HIP_TRY(hipMalloc(&p->ws, need));
-    p->ws_bytes = need;
+  if (need > p->ws_bytes[k]) {
+    if (p->ws[k]) HIP_TRY(hipFree(p->ws[k]));
+    p->ws[k] = nullptr;
+    HIP_TRY(hipMalloc(&p->ws[k], need));
+    p->ws_bytes[k] = need;
   }
-  carve(p, d, reinterpret_cast<char*>(p->ws), p->work);
-  p->dims = d;
-  p->have_work = true;
+  carve(p, d, reinterpret_cast<char*>(p->ws[k]), p->work[k]);
+  p->dims[k] = d;
+  p->have_work[k] = true;
   return KPD_OK;
 }
 
-int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
-                int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis, float* box_scores,
-                int32_t* topk_out, void* stream) {
-  if (!p) return fail(KPD_EINVAL, "null plan");
-  if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
-  if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
-  if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
-  if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD)) return fail(KPD_EINVAL, "unknown flags");
+// One sub-batch of the forward pass on one stream, with workspace k.
+// Arguments are validated by kpd_forward; pointers are already offset to the
+// sub-batch's first image.  Debug buffers are recorded only when debug != 0.
+static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B, int C, int H, int W, float* boxes,
+                       int NB, int P, int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis,
+                       float* box_scores, int32_t* topk_out, hipStream_t st) {
   const bool detect = flags & KPD_FLAG_DETECT, dual = flags & KPD_FLAG_DUAL_HEAD;
-  if (detect && (NB != B || P <= 0 || !boxes)) return fail(KPD_EINVAL, "detect mode: boxes must be [B][P>0][4]");
-  if (detect && !p->anchors) return fail(KPD_ESTATE, "person detector weights missing");
-  if (dual && !p->has_kh) return fail(KPD_ESTATE, "dual head requested but no keypoint_head.* weights");
-  if (dual && NB * P > 0 && (!kh_kpts || !kh_vis)) return fail(KPD_EINVAL, "null dual-head output pointer");
-  if (NB < 0 || NB > B || P < 0) return fail(KPD_EINVAL, "bad box batch");
-  if (NB * P > 0 && (!boxes || !kpts || !vis)) return fail(KPD_EINVAL, "null box/output pointer");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  HIP_TRY(hipSetDevice(p->device));
-
   Dims d;
   d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P; d.flags = flags;
   d.h[0] = (H - 1) / 2 + 1; d.w[0] = (W - 1) / 2 + 1;
@@ -768,13 +777,14 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   const int HWf = d.Hf * d.Wf, TM = split ? conv16_tile_m() : conv_tile_m();
   d.fused_stats = (HWf % TM) == 0;
   d.tiles = d.fused_stats ? HWf / TM : std::min(64, HWf);
-  if (int rc = ensure_work(p, d)) return rc;
-  Work& w = p->work;
-  p->debug.clear();
+  if (int rc = ensure_work(p, d, k)) return rc;
+  Work& w = p->work[k];
+  g_splitk = w.splitk;
+  std::map<std::string, std::pair<const void*, size_t>> dbg;
 
   // ---------------- MobileNetV3-Small body ----------------
   std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
-  if (split) HIP_TRY(hipMemsetAsync(w.sc, 0, 2 * sizeof(float), st));
+  if (split) HIP_TRY(hipMemsetAsync(w.sc, 0, 2 * kAmaxSlots * kAmaxStride * sizeof(float), st));
   HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], split ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
@@ -820,7 +830,7 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
     if (i == 0 && split) return fail(KPD_EINVAL, "split FPN needs the 16-channel stem tap");
     if (int rc = conv(L, taps[i], B, lh[i], lw[i], pad16(kFpnIn[i]), w.lat[i], ACT_NONE, res,
                       i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st,
-                      (i == 1 && split) ? w.sc + 1 : nullptr))
+                      (i == 1 && split) ? w.sc + kAmaxSlots * kAmaxStride : nullptr))
       return rc;
   }
   lat_stage.reset();
@@ -843,12 +853,13 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st));
   topk_stage.reset();
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
-  p->debug["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
-  p->debug["scores"] = {w.scores, sizeof(float) * (size_t)B * 128};
-  p->debug["tap0"] = {taps[0], sizeof(float) * (size_t)B * lh[0] * lw[0] * 16};
-  p->debug["tap1"] = {taps[1], sizeof(float) * (size_t)B * lh[1] * lw[1] * pad16(24)};
-  p->debug["tap2"] = {taps[2], sizeof(float) * (size_t)B * lh[2] * lw[2] * pad16(48)};
-  p->debug["tap3"] = {taps[3], sizeof(float) * (size_t)B * lh[3] * lw[3] * 576};
+  dbg["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
+  dbg["scores"] = {w.scores, sizeof(float) * (size_t)B * 128};
+  dbg["tap0"] = {taps[0], sizeof(float) * (size_t)B * lh[0] * lw[0] * 16};
+  dbg["tap1"] = {taps[1], sizeof(float) * (size_t)B * lh[1] * lw[1] * pad16(24)};
+  dbg["tap2"] = {taps[2], sizeof(float) * (size_t)B * lh[2] * lw[2] * pad16(48)};
+  dbg["tap3"] = {taps[3], sizeof(float) * (size_t)B * lh[3] * lw[3] * 576};
+  if (debug) p->debug = dbg;
 
   // ---------------- person-detector glue (boxes become an output) ----------------
   if (detect) {
@@ -877,7 +888,7 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
     HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, vis, st));
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
   }
-  p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
+  if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
   std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
   HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw, st));
   HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
@@ -946,6 +957,69 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
                             p->kh_fr_b, p->kh_lnv_g, p->kh_lnv_b, p->kh_fv_w, p->kh_fv_b, w.slot, R, P, kh_kpts,
                             kh_vis, st));
   }
+  return KPD_OK;
+}
+
+int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
+                int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis, float* box_scores,
+                int32_t* topk_out, void* stream) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
+  if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
+  if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD)) return fail(KPD_EINVAL, "unknown flags");
+  const bool detect = flags & KPD_FLAG_DETECT, dual = flags & KPD_FLAG_DUAL_HEAD;
+  if (detect && (NB != B || P <= 0 || !boxes)) return fail(KPD_EINVAL, "detect mode: boxes must be [B][P>0][4]");
+  if (detect && !p->anchors) return fail(KPD_ESTATE, "person detector weights missing");
+  if (dual && !p->has_kh) return fail(KPD_ESTATE, "dual head requested but no keypoint_head.* weights");
+  if (dual && NB * P > 0 && (!kh_kpts || !kh_vis)) return fail(KPD_EINVAL, "null dual-head output pointer");
+  if (NB < 0 || NB > B || P < 0) return fail(KPD_EINVAL, "bad box batch");
+  if (NB * P > 0 && (!boxes || !kpts || !vis)) return fail(KPD_EINVAL, "null box/output pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  p->debug.clear();
+
+  // Images are independent (eval BN, per-image ROI loops -- SURVEY §8(e)), so
+  // a large batch runs as S contiguous sub-batches on S streams: the many
+  // small latency-bound launches of one sub-batch (MobileNet body, heads)
+  // overlap the other's.  Sub-batch 0 uses the caller's stream; the others
+  // fork from it and join back before return.  Debug buffers need S == 1.
+  constexpr int kMinSub = 16;
+  const int S = std::max(1, std::min({p->streams, kpd_plan::kMaxSub, B / kMinSub}));
+  if (S == 1)
+    return forward_one(p, 0, true, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis,
+                       box_scores, topk_out, st);
+  if (!p->fork_ev) HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
+  for (int k = 1; k < S; ++k) {
+    if (!p->sub_st[k]) HIP_TRY(hipStreamCreateWithFlags(&p->sub_st[k], hipStreamNonBlocking));
+    if (!p->join_ev[k]) HIP_TRY(hipEventCreateWithFlags(&p->join_ev[k], hipEventDisableTiming));
+  }
+  HIP_TRY(hipEventRecord(p->fork_ev, st));
+  const size_t img_sz = (size_t)C * H * W, per_kp = (size_t)P * 17;
+  int rc = KPD_OK;
+  for (int k = 0; k < S && rc == KPD_OK; ++k) {
+    const int b0 = (int)((long)B * k / S), b1 = (int)((long)B * (k + 1) / S), nb = b1 - b0;
+    const int nbox = std::max(0, std::min(NB, b1) - b0);
+    hipStream_t sk = k ? p->sub_st[k] : st;
+    if (k) HIP_TRY(hipStreamWaitEvent(sk, p->fork_ev, 0));
+    auto off = [&](float* q, size_t per) { return q ? q + (size_t)b0 * per : q; };
+    rc = forward_one(p, k, false, image + (size_t)b0 * img_sz, nb, C, H, W, nbox > 0 || detect ? off(boxes, (size_t)P * 4)
+                                                                                           : nullptr,
+                     nbox, P, flags, off(kpts, per_kp * 2), off(vis, per_kp * 3), off(heat, per_kp * 3136),
+                     off(kh_kpts, per_kp * 2), off(kh_vis, per_kp * 3), off(box_scores, (size_t)P),
+                     topk_out ? topk_out + (size_t)b0 * 64 : nullptr, sk);
+  }
+  for (int k = 1; k < S; ++k) {
+    HIP_TRY(hipEventRecord(p->join_ev[k], p->sub_st[k]));
+    HIP_TRY(hipStreamWaitEvent(st, p->join_ev[k], 0));
+  }
+  return rc;
+}
+
+int kpd_plan_set_streams(kpd_plan* p, int n) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  if (n < 1 || n > kpd_plan::kMaxSub) return fail(KPD_EINVAL, "streams must be in [1, 4]");
+  p->streams = n;
   return KPD_OK;
 }
 

@@ -22,7 +22,8 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "mixed": KPD_PRECISION_MIXED, "bf16": 
 # every symbol include/kpd.h declares (checked by tests/test_abi.py)
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
-           "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector")
+           "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector", "kpd_bench_conv16",
+           "kpd_plan_set_streams")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",
@@ -120,6 +121,10 @@ class Plan:
     def set_detector(self, conf_threshold: float, nms_iou_threshold: float) -> None:
         check(self.lib.kpd_plan_set_detector(self.h, float(conf_threshold), float(nms_iou_threshold)),
               "kpd_plan_set_detector")
+
+    def set_streams(self, n: int) -> None:
+        """Sub-batch streams for large batches (kpd_plan_set_streams)."""
+        check(self.lib.kpd_plan_set_streams(self.h, int(n)), "kpd_plan_set_streams")
 
     def forward(self, image: torch.Tensor, boxes: Optional[torch.Tensor], kpts, vis, heat, flags: int = 0,
                 kh_kpts=None, kh_vis=None, box_scores=None, topk=None) -> None:

@@ -78,7 +78,7 @@ class MultiPersonKeypointModel(nn.Module):
     """
 
     def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "fp32",
-                 dual_head: bool = False, max_persons: int = 5):
+                 dual_head: bool = False, max_persons: int = 5, streams: int = 2):
         super().__init__()
         if precision not in _native.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_native.PRECISIONS)}")
@@ -94,6 +94,7 @@ class MultiPersonKeypointModel(nn.Module):
         self.max_persons = max_persons
         self.num_keypoints = config.num_keypoints
         self.precision = precision
+        self.streams = streams          # sub-batch streams for B >= 32 (kpd_plan_set_streams)
         self._plan: Optional[_native.Plan] = None
         self._plan_key = None
         if config.num_keypoints != 17 or config.heatmap_head.in_channels != 64 \
@@ -103,7 +104,7 @@ class MultiPersonKeypointModel(nn.Module):
     # ------------------------------------------------------------------ plan
     def _weights_key(self, device: torch.device) -> Tuple:
         vers = tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
-        return (device, self.precision, vers)
+        return (device, self.precision, self.streams, vers)
 
     def native_plan(self, device: torch.device) -> _native.Plan:
         """Build (or reuse) the packed-weight plan for ``device``."""
@@ -116,6 +117,7 @@ class MultiPersonKeypointModel(nn.Module):
             plan.finalize(_native.PRECISIONS[self.precision])
             ph = self.config.person_head
             plan.set_detector(ph.conf_threshold, ph.nms_iou_threshold)
+            plan.set_streams(self.streams)
             self._plan, self._plan_key = plan, key
         return self._plan
 

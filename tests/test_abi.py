@@ -12,7 +12,7 @@ from conftest import ROOT
 
 def _declared():
     hdr = (ROOT / "include" / "kpd.h").read_text()
-    return sorted(set(re.findall(r"\b(kpd_[a-z_]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(kpd_[a-z0-9_]+)\s*\(", hdr)))
 
 
 def test_header_matches_binding():

@@ -266,3 +266,28 @@ def test_predict_cli(tmp_path, capsys):
     txt = capsys.readouterr().out
     assert "Keypoints shape: (2, 17, 2)" in txt
     assert " 1. nose" in txt and "17. right_ankle" in txt
+
+
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_sub_batch_streams_match(model_sd, precision):
+    """kpd_forward splits B >= 32 over sub-batch streams: same outputs as one
+    stream (bit-identical in fp32; the mixed FPN scale is per sub-batch)."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(48, 3, 256, 192, seed=41, device=DEV)
+    boxes = synthetic_boxes(48, 2, seed=42, device=DEV)
+    boxes[5, 1] = 0.0                       # a zero box inside the second sub-batch
+    outs = []
+    for streams in (1, 3):
+        m = _model(model_sd, precision)
+        m.streams = streams
+        with torch.no_grad():
+            outs.append(m({"image": img, "bboxes": boxes}))
+    a, b = outs
+    if precision == "fp32":
+        assert torch.equal(a["keypoints"], b["keypoints"]) and torch.equal(a["heatmap"], b["heatmap"])
+        assert torch.equal(a["visibilities"], b["visibilities"])
+    else:
+        # the split FPN scale is per sub-batch: ~1e-7 relative in feat0, which the
+        # bf16 heatmap head can turn into a bf16 ulp here and there
+        torch.testing.assert_close(a["keypoints"], b["keypoints"], atol=1e-3, rtol=0)
+        torch.testing.assert_close(a["heatmap"], b["heatmap"], atol=3e-2, rtol=0)

@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Ablation timings of the LDS-DMA conv (kpd_bench_conv16): full kernel, no
+K-loop loads, no MFMAs, L2-resident A.  Prints one JSON line per case."""
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "keypoint-detection_amd"))
+from dll import _native  # noqa: E402
+
+lib = _native.load()
+CASES = [  # (label, split, N, H, W, cin, cout, flop)
+    ("fpn0_split", 1, 64, 128, 96, 128, 128, 2 * 64 * 128 * 96 * 128 * 128 * 9 * 3),
+    ("hm2_bf16", 0, 64, 56, 56, 256, 256, 2 * 64 * 56 * 56 * 256 * 256 * 9),
+]
+for label, split, N, H, W, cin, cout, flop in CASES:
+    for dbg in (0, 1, 2, 4):
+        ms = ctypes.c_float(0)
+        rc = lib.kpd_bench_conv16(split, N, H, W, cin, cout, dbg, 20, ctypes.byref(ms))
+        print(json.dumps({"case": label, "dbg": dbg, "rc": rc, "ms": round(ms.value, 4),
+                          "mfma_tflops": round(flop / (ms.value * 1e-3) / 1e12, 1) if rc == 0 and ms.value else None}),
+              flush=True)
