@@ -64,38 +64,60 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
   }
 }
 
-template <int K, int S>
+// Depthwise KxK conv, stride S, "same" padding, + folded BN + act.  A thread
+// owns 4 channels (one 16-byte quad) x XT consecutive output columns: each
+// input column loaded feeds up to ceil(K/S) outputs from registers, so a 5x5
+// stride-1 row costs 8 loads for 4 outputs instead of 20.
+template <int K, int S, int XT = 4>
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ in, const float* __restrict__ w,
                                                      const float* __restrict__ b, float* __restrict__ out,
                                                      int N, int H, int W, int Cp, int Ho, int Wo, int act) {
-  const int nq = Cp >> 2;
+  constexpr int P = (K - 1) / 2, NC = (XT - 1) * S + K;   // input columns per row
+  const int nq = Cp >> 2, wx = (Wo + XT - 1) / XT;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)N * Ho * Wo * nq;
+  const size_t total = (size_t)N * Ho * wx * nq;
   if (idx >= total) return;
   const int q = idx % nq;
-  const size_t pix = idx / nq;
-  const int n = pix / (Ho * Wo), r = pix - (size_t)n * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
-  constexpr int P = (K - 1) / 2;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const size_t rest = idx / nq;
+  const int xt = rest % wx;
+  const int nr = rest / wx, n = nr / Ho, oy = nr - n * Ho, ox0 = xt * XT;
+  const int ix0 = ox0 * S - P;
+  float4 acc[XT];
+#pragma unroll
+  for (int o = 0; o < XT; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int ky = 0; ky < K; ++ky) {
     const int iy = oy * S - P + ky;
     if (iy < 0 || iy >= H) continue;
+    const float* row = in + ((size_t)(n * H + iy) * W) * Cp + q * 4;
+    float4 col[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ix = ix0 + c;
+      col[c] = (ix >= 0 && ix < W) ? *reinterpret_cast<const float4*>(row + (size_t)ix * Cp)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int kx = 0; kx < K; ++kx) {
-      const int ix = ox * S - P + kx;
-      if (ix < 0 || ix >= W) continue;
-      const float4 v = *reinterpret_cast<const float4*>(in + ((size_t)(n * H + iy) * W + ix) * Cp + q * 4);
       const float4 k = *reinterpret_cast<const float4*>(w + (ky * K + kx) * Cp + q * 4);
-      acc.x = fmaf(v.x, k.x, acc.x); acc.y = fmaf(v.y, k.y, acc.y);
-      acc.z = fmaf(v.z, k.z, acc.z); acc.w = fmaf(v.w, k.w, acc.w);
+#pragma unroll
+      for (int o = 0; o < XT; ++o) {
+        const float4 v = col[o * S + kx];
+        acc[o].x = fmaf(v.x, k.x, acc[o].x); acc[o].y = fmaf(v.y, k.y, acc[o].y);
+        acc[o].z = fmaf(v.z, k.z, acc[o].z); acc[o].w = fmaf(v.w, k.w, acc[o].w);
+      }
     }
   }
   const float4 bb = *reinterpret_cast<const float4*>(b + q * 4);
-  float4 o;
-  o.x = kpd_act(acc.x + bb.x, act); o.y = kpd_act(acc.y + bb.y, act);
-  o.z = kpd_act(acc.z + bb.z, act); o.w = kpd_act(acc.w + bb.w, act);
-  *reinterpret_cast<float4*>(out + pix * Cp + q * 4) = o;
+  float* op = out + ((size_t)(n * Ho + oy) * Wo + ox0) * Cp + q * 4;
+#pragma unroll
+  for (int o = 0; o < XT; ++o) {
+    if (ox0 + o >= Wo) break;
+    float4 r;
+    r.x = kpd_act(acc[o].x + bb.x, act); r.y = kpd_act(acc[o].y + bb.y, act);
+    r.z = kpd_act(acc[o].z + bb.z, act); r.w = kpd_act(acc[o].w + bb.w, act);
+    *reinterpret_cast<float4*>(op + (size_t)o * Cp) = r;
+  }
 }
 
 // Squeeze-excitation, one 1024-thread workgroup (16 waves) per image: the
@@ -192,22 +214,25 @@ __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict_
 }
 
 // FPN lateral 1x1 conv with a small input width (cin_p <= 32) and 128 outputs,
-// plus the nearest-upsampled top-down residual (backbone.py:33-37) and the
-// max|out| the split16 FPN conv needs.  Pure streaming: one 16-byte store per
-// thread, weights transposed in LDS, the input pixel broadcast to the 32
-// threads that produce its 128 outputs.  64 pixels per workgroup.
-__global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __restrict__ in, int cin_p,
+// plus the nearest-upsampled top-down residual (backbone.py:33-37).  Pure
+// streaming (it writes the largest tensor of the pass): a thread owns 8 output
+// channels of 4 pixels, every input of the 4 pixels is loaded before the first
+// store, and every store is 16 bytes.  Weights transposed in LDS.  64 pixels
+// per workgroup.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
+// 32 channels per [hi32 | lo32] 128-byte group (the split FPN conv's K row).
+constexpr int kLatPix = 4;   // pixels per thread
+template <int CIN4>          // cin_p / 4
+__global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __restrict__ in,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ res, int H, int W, int rh,
                                                              int rw, int M, float* __restrict__ out,
                                                              float* __restrict__ amax, const float* __restrict__ sc_in,
                                                              float maxb, float maxs) {
-  __shared__ float sw[32 * 128];
+  __shared__ __attribute__((aligned(16))) float sw[32 * 128];
   __shared__ float red[4];
   const int tid = threadIdx.x;
-  // split output (sc_in != null): x * 2^a_exp as f16 hi + lo, 32 channels per
-  // [hi32 | lo32] 128-byte group -- the K-tile row of the split FPN conv
+  constexpr int cin_p = CIN4 * 4;
   float sa = 1.f;
   if (sc_in) sa = ldexpf(1.f, split_a_exp(sc_in, maxb, maxs));
   for (int i = tid; i < cin_p * 128; i += 256) {
@@ -215,47 +240,72 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
     sw[k * 128 + co] = w[i];
   }
   __syncthreads();
-  const int c4 = tid & 31, sub = tid >> 5, co = c4 * 4;
-  const float4 b = *reinterpret_cast<const float4*>(bias + co);
+  const int c8 = tid & 15, sub = tid >> 4, co = c8 * 8;
+  const float4 b0 = *reinterpret_cast<const float4*>(bias + co), b1 = *reinterpret_cast<const float4*>(bias + co + 4);
   const int HW = H * W;
   const float sy = (float)rh / (float)H, sx = (float)rw / (float)W;
-  float m_abs = 0.f;
-  for (int it = 0; it < 8; ++it) {
-    const int m = blockIdx.x * 64 + it * 8 + sub;
-    if (m >= M) break;
-    const float* ip = in + (size_t)m * cin_p;
-    float4 acc = b;
-    for (int k = 0; k < cin_p; k += 4) {
-      const float4 x = *reinterpret_cast<const float4*>(ip + k);
-      const float xs[4] = {x.x, x.y, x.z, x.w};
+  // load phase: inputs and residuals of this thread's 4 pixels
+  float4 xin[kLatPix][CIN4];
+  float4 r0[kLatPix], r1[kLatPix];
+  int mm[kLatPix];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 wv = *reinterpret_cast<const float4*>(sw + (k + q) * 128 + co);
-        acc.x = fmaf(xs[q], wv.x, acc.x); acc.y = fmaf(xs[q], wv.y, acc.y);
-        acc.z = fmaf(xs[q], wv.z, acc.z); acc.w = fmaf(xs[q], wv.w, acc.w);
-      }
-    }
+  for (int it = 0; it < kLatPix; ++it) {
+    const int m = blockIdx.x * 64 + it * 16 + sub;
+    mm[it] = m;
+    r0[it] = r1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < CIN4; ++k) xin[it][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m >= M) continue;
+#pragma unroll
+    for (int k = 0; k < CIN4; ++k) xin[it][k] = *reinterpret_cast<const float4*>(in + (size_t)m * cin_p + k * 4);
     if (res) {
       const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
       const int yy = rh == H ? y : min((int)floorf((float)y * sy), rh - 1);
       const int xx = rw == W ? x : min((int)floorf((float)x * sx), rw - 1);
-      const float4 q = *reinterpret_cast<const float4*>(res + ((size_t)(n * rh + yy) * rw + xx) * 128 + co);
-      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+      const float* rp = res + ((size_t)(n * rh + yy) * rw + xx) * 128 + co;
+      r0[it] = *reinterpret_cast<const float4*>(rp);
+      r1[it] = *reinterpret_cast<const float4*>(rp + 4);
     }
-    m_abs = fmaxf(m_abs, fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fmaxf(fabsf(acc.z), fabsf(acc.w))));
-    if (sc_in) {
-      const float xs[4] = {acc.x * sa, acc.y * sa, acc.z * sa, acc.w * sa};
-      f16x4 hi, lo;
+  }
+  float m_abs = 0.f;
+#pragma unroll
+  for (int it = 0; it < kLatPix; ++it) {
+    const int m = mm[it];
+    if (m >= M) continue;
+    float a[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int k4 = 0; k4 < CIN4; ++k4) {
+      const float xs[4] = {xin[it][k4].x, xin[it][k4].y, xin[it][k4].z, xin[it][k4].w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        hi[q] = (_Float16)xs[q];
-        lo[q] = (_Float16)(xs[q] - (float)hi[q]);
+        const float4 w0 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co);
+        const float4 w1 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co + 4);
+        a[0] = fmaf(xs[q], w0.x, a[0]); a[1] = fmaf(xs[q], w0.y, a[1]);
+        a[2] = fmaf(xs[q], w0.z, a[2]); a[3] = fmaf(xs[q], w0.w, a[3]);
+        a[4] = fmaf(xs[q], w1.x, a[4]); a[5] = fmaf(xs[q], w1.y, a[5]);
+        a[6] = fmaf(xs[q], w1.z, a[6]); a[7] = fmaf(xs[q], w1.w, a[7]);
+      }
+    }
+    a[0] += r0[it].x; a[1] += r0[it].y; a[2] += r0[it].z; a[3] += r0[it].w;
+    a[4] += r1[it].x; a[5] += r1[it].y; a[6] += r1[it].z; a[7] += r1[it].w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m_abs = fmaxf(m_abs, fabsf(a[e]));
+    if (sc_in) {
+      typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+      f16x8v hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xsc = a[e] * sa;
+        hi[e] = (_Float16)xsc;
+        lo[e] = (_Float16)(xsc - (float)hi[e]);
       }
       _Float16* o16 = reinterpret_cast<_Float16*>(out) + (size_t)m * 256 + (co >> 5) * 64 + (co & 31);
-      *reinterpret_cast<f16x4*>(o16) = hi;
-      *reinterpret_cast<f16x4*>(o16 + 32) = lo;
+      *reinterpret_cast<f16x8v*>(o16) = hi;
+      *reinterpret_cast<f16x8v*>(o16 + 32) = lo;
     } else {
-      *reinterpret_cast<float4*>(out + (size_t)m * 128 + co) = acc;
+      float* op = out + (size_t)m * 128 + co;
+      *reinterpret_cast<float4*>(op) = make_float4(a[0], a[1], a[2], a[3]);
+      *reinterpret_cast<float4*>(op + 4) = make_float4(a[4], a[5], a[6], a[7]);
     }
   }
   if (amax) {
@@ -299,7 +349,7 @@ hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const flo
 
 hipError_t launch_dwconv(const float* in, const float* w, const float* b, float* out, int N, int H, int W,
                          int Cp, int Ho, int Wo, int k, int s, int act, hipStream_t st) {
-  const size_t total = (size_t)N * Ho * Wo * (Cp / 4);
+  const size_t total = (size_t)N * Ho * ((Wo + 3) / 4) * (Cp / 4);
   const dim3 grid((unsigned)((total + 255) / 256));
 #define DW(K, S) hipLaunchKernelGGL((dwconv_kernel<K, S>), grid, dim3(256), 0, st, in, w, b, out, N, H, W, Cp, Ho, Wo, act)
   if (k == 3 && s == 1) DW(3, 1);
@@ -321,10 +371,16 @@ hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* 
 hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
                                  int N, int H, int W, int rh, int rw, void* out, float* amax, const float* sc_in,
                                  float maxb, float maxs, hipStream_t st) {
-  if (cin_p > 32 || cin_p % 4) return hipErrorInvalidValue;
+  if (cin_p != 16 && cin_p != 32) return hipErrorInvalidValue;
   const int M = N * H * W;
-  hipLaunchKernelGGL(lateral_stream_kernel, dim3((M + 63) / 64), dim3(256), 0, st, in, cin_p, w, bias, res, H, W, rh,
-                     rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs);
+#define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3((M + 63) / 64), dim3(256), 0, st, in, w, bias, res, H, \
+                                  W, rh, rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs)
+  switch (cin_p / 4) {
+    case 4: LAT(4); break;
+    case 8: LAT(8); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LAT
   return hipGetLastError();
 }
 

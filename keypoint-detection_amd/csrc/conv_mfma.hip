@@ -53,7 +53,11 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   static_assert(ROWB % 64 == 0, "BK must cover 64 bytes");
 
   constexpr int MAIN_LDS = 2 * (BUF_A + BUF_B);
-  constexpr int EPI_LDS = epi_lds_bytes<BM, BN>();
+  // BN = 128: the epilogue stages one 64-column half at a time (the two wave
+  // columns in turn), halving its LDS -- the occupancy limiter of the
+  // latency-bound small-K 1x1 convs
+  constexpr int EBN = BN == 128 ? 64 : BN, HALVES = BN / EBN;
+  constexpr int EPI_LDS = epi_lds_bytes<BM, EBN>();
   __shared__ __attribute__((aligned(16))) char lds[MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS];
   char* As = lds;
   char* Bs = lds + 2 * BUF_A;
@@ -232,25 +236,31 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
 
   // ---------------- epilogue (LDS-staged, 16-byte row stores) ----------------
   float* tile = reinterpret_cast<float*>(lds);
-  acc_to_lds<FM, FN, WM, WN, BN>(tile, acc, wm, wn, lane);
-  if (p.k_split > 1) {   // raw partial sums; splitk_reduce_kernel applies the epilogue
-    constexpr int P = BN + 4, C4 = BN / 4;
-    __syncthreads();
-    float* dst = p.splitk_ws + (size_t)ks * M * cout_p;
-    for (int idx = tid; idx < BM * C4; idx += 256) {
-      const int row = idx / C4, c4 = idx - row * C4, m = m0 + row, co = n0 + c4 * 4;
-      if (m < M && co < cout_p)
-        *reinterpret_cast<float4*>(dst + (size_t)m * cout_p + co) =
-            *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
-    }
-    return;
-  }
-  EpiArgs e;
+  EpiArgs e{};
   e.bias = p.bias; e.out = p.out; e.res = p.res; e.stats = p.stats; e.amax = p.amax; e.scale = 1.f;
   e.M = M; e.H = H; e.W = W; e.cout_p = cout_p; e.out_cstride = p.out_cstride; e.rh = p.rh; e.rw = p.rw;
   e.act = p.act; e.tiles_per_img = p.tiles_per_img;
   e.post_scale = p.post_scale; e.post_shift = p.post_shift; e.act2 = p.act2; e.act3 = p.act3;
-  tile_store<TO, BM, BN>(tile, e, m0, n0);
+#pragma unroll
+  for (int h = 0; h < HALVES; ++h) {
+    if (h) __syncthreads();
+    if constexpr (HALVES == 1) acc_to_lds<FM, FN, WM, WN, BN>(tile, acc, wm, wn, lane);
+    else if (wn == h) acc_to_lds<FM, FN, WM, WN, EBN>(tile, acc, wm, 0, lane);
+    const int nh = n0 + h * EBN;
+    if (p.k_split > 1) {   // raw partial sums; splitk_reduce_kernel applies the epilogue
+      constexpr int P = EBN + 4, C4 = EBN / 4;
+      __syncthreads();
+      float* dst = p.splitk_ws + (size_t)ks * M * cout_p;
+      for (int idx = tid; idx < BM * C4; idx += 256) {
+        const int row = idx / C4, c4 = idx - row * C4, m = m0 + row, co = nh + c4 * 4;
+        if (m < M && co < cout_p)
+          *reinterpret_cast<float4*>(dst + (size_t)m * cout_p + co) =
+              *reinterpret_cast<const float4*>(tile + row * P + c4 * 4);
+      }
+      continue;
+    }
+    tile_store<TO, BM, EBN>(tile, e, m0, nh);
+  }
 }
 
 // Split-K reduction + the conv epilogue (bias, act, second affine, residual
