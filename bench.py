@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="sub-batch streams inside one forward (kpd_plan_set_streams)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")

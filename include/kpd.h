@@ -118,8 +118,10 @@ int kpd_nms(const float* boxes, const float* scores, int n, float iou_threshold,
 /* Concurrency: a forward pass over B >= 32 images runs as min(n, B/16)
  * contiguous sub-batches on as many streams (forked from / joined back into
  * the caller's stream), so the latency-bound small launches of one sub-batch
- * overlap the other's.  n in [1, 4]; default 2.  Results do not depend on n
- * beyond fp32 rounding in the mixed-precision FPN scale. */
+ * overlap the other's.  n in [1, 4]; default 1 (n = 2 measured +4% images/s at
+ * C2, but every kernel then shares the GPU with the other sub-batch, so
+ * per-kernel timings no longer describe the kernel).  Results do not depend
+ * on n beyond fp32 rounding in the mixed-precision FPN scale. */
 int kpd_plan_set_streams(kpd_plan* plan, int n);
 
 /* Diagnostics (not part of the reference interface): times the LDS-DMA 3x3

@@ -216,11 +216,11 @@ __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict_
 // FPN lateral 1x1 conv with a small input width (cin_p <= 32) and 128 outputs,
 // plus the nearest-upsampled top-down residual (backbone.py:33-37).  Pure
 // streaming (it writes the largest tensor of the pass): a thread owns 8 output
-// channels of 4 pixels, every input of the 4 pixels is loaded before the first
-// store, and every store is 16 bytes.  Weights transposed in LDS.  64 pixels
-// per workgroup.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
+// channels of kLatPix pixels, all their inputs are loaded before the first
+// store, and every store is 16 bytes.  Weights transposed in LDS.  16 x
+// kLatPix pixels per workgroup.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
 // 32 channels per [hi32 | lo32] 128-byte group (the split FPN conv's K row).
-constexpr int kLatPix = 4;   // pixels per thread
+constexpr int kLatPix = 2;   // pixels per thread (4 doubles the registers and halves occupancy: slower)
 template <int CIN4>          // cin_p / 4
 __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __restrict__ in,
                                                              const float* __restrict__ w,
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
   int mm[kLatPix];
 #pragma unroll
   for (int it = 0; it < kLatPix; ++it) {
-    const int m = blockIdx.x * 64 + it * 16 + sub;
+    const int m = blockIdx.x * (16 * kLatPix) + it * 16 + sub;
     mm[it] = m;
     r0[it] = r1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -373,7 +373,7 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
                                  float maxb, float maxs, hipStream_t st) {
   if (cin_p != 16 && cin_p != 32) return hipErrorInvalidValue;
   const int M = N * H * W;
-#define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3((M + 63) / 64), dim3(256), 0, st, in, w, bias, res, H, \
+#define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3((M + 16 * kLatPix - 1) / (16 * kLatPix)), dim3(256), 0, st, in, w, bias, res, H, \
                                   W, rh, rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs)
   switch (cin_p / 4) {
     case 4: LAT(4); break;

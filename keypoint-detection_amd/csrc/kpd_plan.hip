@@ -177,7 +177,7 @@ struct kpd_plan {
   Dims dims[kMaxSub];
   Work work[kMaxSub];
   bool have_work[kMaxSub] = {};
-  int streams = 2;                        // requested sub-batch streams
+  int streams = 1;                        // requested sub-batch streams (kpd_plan_set_streams)
   hipStream_t sub_st[kMaxSub] = {};       // [0] unused: sub-batch 0 runs on the caller's stream
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::map<std::string, std::pair<const void*, size_t>> debug;

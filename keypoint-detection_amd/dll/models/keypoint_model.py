@@ -78,7 +78,7 @@ class MultiPersonKeypointModel(nn.Module):
     """
 
     def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "fp32",
-                 dual_head: bool = False, max_persons: int = 5, streams: int = 2):
+                 dual_head: bool = False, max_persons: int = 5, streams: int = 1):
         super().__init__()
         if precision not in _native.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_native.PRECISIONS)}")
