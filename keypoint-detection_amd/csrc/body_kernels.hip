@@ -10,6 +10,8 @@
 //     A-load (conv_mfma.hip, a_scale), so the scaled tensor never hits HBM.
 //   * channel_stats: per-image channel sum/max partials for ChannelAttention
 //     when the FPN conv epilogue cannot produce them (H*W not a tile multiple).
+#include <algorithm>
+
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 
@@ -120,6 +122,142 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ i
   }
 }
 
+// Fused MobileNetV3 inverted-residual front half for the coarse maps:
+// expand 1x1 (+ folded BN + act) -> depthwise KxK stride S (+ folded BN + act)
+// -> output, plus the per-image channel means the SE block needs.  One
+// workgroup per (image, slice of CS expanded channels): the whole input image
+// is staged in LDS once, the expanded slice never leaves LDS (no HBM round
+// trip, one launch instead of two, and the SE pooling pass disappears).  The
+// depthwise zero padding is the LDS image's border test.  Channel means are
+// reduced in a fixed order (deterministic).  torchvision InvertedResidual
+// (backbone.py:250-254 via mobilenet_v3_small).
+template <int K, int S>
+__global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = blockIdx.y, c0 = blockIdx.x * p.CS, tid = threadIdx.x;
+  const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, CS = p.CS, cq = CS / 4, cin_p = p.cin_p;
+  // LDS: [weT: cin_p x CS] [es: Pin x CS] [wds: K*K x CS] [ds: Po x CS, the means]
+  float* weT = sm;
+  float* es = weT + (p.we ? cin_p * CS : 0);
+  float* wds = es + Pin * CS;
+  float* ds = wds + K * K * CS;
+  const float* xg = p.x + (size_t)n * Pin * cin_p;
+  if (p.we) {
+    for (int i = tid; i < cin_p * CS; i += 256) {   // transposed weight slice: weT[k][c]
+      const int c = i / cin_p, k = i - c * cin_p;
+      weT[k * CS + c] = p.we[(size_t)(c0 + c) * cin_p + k];
+    }
+  } else {   // no expand (exp == cin): the slice of x is the depthwise input
+    for (int i = tid; i < Pin * cq; i += 256) {
+      const int px = i / cq, q = i - px * cq;
+      reinterpret_cast<float4*>(es)[i] = *reinterpret_cast<const float4*>(xg + (size_t)px * cin_p + c0 + q * 4);
+    }
+  }
+  for (int i = tid; i < K * K * cq; i += 256) {
+    const int t = i / cq, q = i - t * cq;
+    reinterpret_cast<float4*>(wds)[i] = *reinterpret_cast<const float4*>(p.wd + (size_t)t * p.Ep + c0 + q * 4);
+  }
+  __syncthreads();
+  if (p.we) {
+    // expand, register-tiled 4 pixels x 4 channels: x rows straight from
+    // global/L1 (shared by the slice's cq threads), weights from LDS
+    const int pg_n = (Pin + 3) / 4;
+    for (int i = tid; i < pg_n * cq; i += 256) {
+      const int pg = i / cq, q = i - pg * cq;
+      const float4 b = *reinterpret_cast<const float4*>(p.be + c0 + q * 4);
+      float a[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { a[r][0] = b.x; a[r][1] = b.y; a[r][2] = b.z; a[r][3] = b.w; }
+      const float* xr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xr[r] = xg + (size_t)min(pg * 4 + r, Pin - 1) * cin_p;
+      for (int k = 0; k < cin_p; k += 4) {
+        float4 xv[4], wv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4*>(xr[r] + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = *reinterpret_cast<const float4*>(weT + (k + j) * CS + q * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xs[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[r][0] = fmaf(xs[j], wv[j].x, a[r][0]); a[r][1] = fmaf(xs[j], wv[j].y, a[r][1]);
+            a[r][2] = fmaf(xs[j], wv[j].z, a[r][2]); a[r][3] = fmaf(xs[j], wv[j].w, a[r][3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = pg * 4 + r;
+        if (px < Pin)
+          reinterpret_cast<float4*>(es)[px * cq + q] =
+              make_float4(kpd_act(a[r][0], p.act_e), kpd_act(a[r][1], p.act_e), kpd_act(a[r][2], p.act_e),
+                          kpd_act(a[r][3], p.act_e));
+      }
+    }
+    __syncthreads();
+  }
+  // depthwise from LDS, 4 consecutive output columns per thread (input columns
+  // reused from registers as in dwconv_kernel)
+  constexpr int PD = (K - 1) / 2, XT = 4, NC = (XT - 1) * S + K;
+  const int wx = (p.Wo + XT - 1) / XT;
+  for (int i = tid; i < p.Ho * wx * cq; i += 256) {
+    const int q = i % cq, r = i / cq, xt = r % wx, oy = r / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
+    float4 a[XT];
+#pragma unroll
+    for (int o = 0; o < XT; ++o) a[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int iy = oy * S - PD + ky;
+      if (iy < 0 || iy >= p.Hi) continue;
+      float4 col[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ix = ix0 + c;
+        col[c] = (ix >= 0 && ix < p.Wi) ? reinterpret_cast<const float4*>(es)[(iy * p.Wi + ix) * cq + q]
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const float4 w = reinterpret_cast<const float4*>(wds)[(ky * K + kx) * cq + q];
+#pragma unroll
+        for (int o = 0; o < XT; ++o) {
+          const float4 v = col[o * S + kx];
+          a[o].x = fmaf(v.x, w.x, a[o].x); a[o].y = fmaf(v.y, w.y, a[o].y);
+          a[o].z = fmaf(v.z, w.z, a[o].z); a[o].w = fmaf(v.w, w.w, a[o].w);
+        }
+      }
+    }
+    const float4 b = *reinterpret_cast<const float4*>(p.bd + c0 + q * 4);
+#pragma unroll
+    for (int o = 0; o < XT; ++o) {
+      if (ox0 + o >= p.Wo) break;
+      float4 v;
+      v.x = kpd_act(a[o].x + b.x, p.act_d); v.y = kpd_act(a[o].y + b.y, p.act_d);
+      v.z = kpd_act(a[o].z + b.z, p.act_d); v.w = kpd_act(a[o].w + b.w, p.act_d);
+      const int op = oy * p.Wo + ox0 + o;
+      *reinterpret_cast<float4*>(p.out + ((size_t)n * Po + op) * p.Ep + c0 + q * 4) = v;
+      if (p.pooled) reinterpret_cast<float4*>(ds)[op * cq + q] = v;
+    }
+  }
+  if (p.pooled) {   // channel means: 256/CS row groups in parallel, then a fixed-order combine
+    __syncthreads();
+    const int groups = 256 / CS, c = tid % CS, g = tid / CS;
+    float sum = 0.f;
+    if (g < groups)
+      for (int op = g; op < Po; op += groups) sum += ds[op * CS + c];
+    __syncthreads();
+    if (g < groups) ds[g * CS + c] = sum;
+    __syncthreads();
+    if (tid < CS) {
+      float t = 0.f;
+      for (int gg = 0; gg < groups; ++gg) t += ds[gg * CS + tid];
+      p.pooled[(size_t)n * p.Ep + c0 + tid] = t / (float)Po;
+    }
+  }
+}
+
 // Squeeze-excitation, one 1024-thread workgroup (16 waves) per image: the
 // three steps are dependent, so each is laid out for memory-level parallelism
 // (all of a step's loads in flight together) rather than per-thread loops.
@@ -130,7 +268,8 @@ constexpr int kSeThreads = 1024;
 __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict__ x, int HW, int C, int Cp,
                                                         const float* __restrict__ w1, const float* __restrict__ b1,
                                                         const float* __restrict__ w2t, const float* __restrict__ b2,
-                                                        int sq, float* __restrict__ scale) {
+                                                        int sq, float* __restrict__ scale,
+                                                        const float* __restrict__ pooled) {
   __shared__ float4 part[kSeThreads];
   __shared__ __attribute__((aligned(16))) float mean[1024];
   __shared__ float hid[256];
@@ -138,6 +277,10 @@ __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict_
   const int nq = Cp >> 2;                       // <= 256
   const int groups = kSeThreads / nq;           // pixel groups sharing a channel quad
   const float* xb = x + (size_t)n * HW * Cp;
+  if (pooled) {   // means already reduced by the fused expand+depthwise kernel
+    for (int c = tid; c < Cp; c += kSeThreads) mean[c] = pooled[(size_t)n * Cp + c];
+    __syncthreads();
+  } else {
   // (1) pool: thread (q, g) sums pixels g, g + groups, ... -- loads independent
   {
     const int q = tid % nq, g = tid / nq;
@@ -169,6 +312,7 @@ __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict_
     *reinterpret_cast<float4*>(mean + tid * 4) = make_float4(t.x / hw, t.y / hw, t.z / hw, t.w / hw);
   }
   __syncthreads();
+  }
   // (2) fc1 + ReLU: wave per output row, lanes split K with 16-byte loads;
   // up to 3 rows x 4 K-chunks (C <= 1024) issued before the reductions
   const int nch = (C + 255) / 256;
@@ -362,9 +506,9 @@ hipError_t launch_dwconv(const float* in, const float* w, const float* b, float*
 }
 
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
-                     const float* w2, const float* b2, int sq, float* scale, hipStream_t st) {
+                     const float* w2, const float* b2, int sq, float* scale, hipStream_t st, const float* pooled) {
   if (Cp > 1024 || sq > 256 || C % 4 || sq % 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(se_kernel, dim3(N), dim3(kSeThreads), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale);
+  hipLaunchKernelGGL(se_kernel, dim3(N), dim3(kSeThreads), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale, pooled);
   return hipGetLastError();
 }
 
@@ -387,5 +531,26 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st) {
   hipLaunchKernelGGL(channel_stats_kernel, dim3(tiles, N), dim3(128), 0, st, x, HW, Cp, tiles, stats);
+  return hipGetLastError();
+}
+
+size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
+  const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
+  return 4 * ((a.we ? (size_t)a.cin_p * a.CS : 0) + (size_t)Pin * a.CS + (size_t)K * K * a.CS +
+              (a.pooled ? (size_t)Po * a.CS : 0));
+}
+
+hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
+  if (a.CS % 4 || a.Ep % a.CS || a.cin_p % 4) return hipErrorInvalidValue;
+  const size_t lds = exdw_lds_bytes(a, K);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(a.Ep / a.CS, N);
+#define EXDW(KK, SS) hipLaunchKernelGGL((exdw_kernel<KK, SS>), grid, dim3(256), lds, st, a)
+  if (K == 3 && S == 1) EXDW(3, 1);
+  else if (K == 3 && S == 2) EXDW(3, 2);
+  else if (K == 5 && S == 1) EXDW(5, 1);
+  else if (K == 5 && S == 2) EXDW(5, 2);
+  else return hipErrorInvalidValue;
+#undef EXDW
   return hipGetLastError();
 }

@@ -61,7 +61,25 @@ hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const flo
 hipError_t launch_dwconv(const float* in, const float* w, const float* b, float* out, int N, int H, int W,
                          int Cp, int Ho, int Wo, int k, int s, int act, hipStream_t st);
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
-                     const float* w2, const float* b2, int sq, float* scale, hipStream_t st);
+                     const float* w2, const float* b2, int sq, float* scale, hipStream_t st,
+                     const float* pooled = nullptr);
+// fused expand 1x1 + depthwise + channel means (body_kernels.hip, exdw_kernel)
+struct ExDwArgs {
+  const float* x;        // NHWC [N][Hi][Wi][cin_p]
+  int Hi, Wi, cin_p;
+  const float* we;       // expand [Ep][cin_p] (BN folded); null: no expand (Ep == cin_p)
+  const float* be;
+  int act_e;
+  const float* wd;       // depthwise [K*K][Ep] (BN folded), bias bd [Ep]
+  const float* bd;
+  int act_d, Ep;
+  float* out;            // [N][Ho][Wo][Ep]
+  int Ho, Wo;
+  float* pooled;         // optional [N][Ep] channel means of out (SE squeeze)
+  int CS;                // expanded channels per workgroup (multiple of 4, divides Ep)
+};
+size_t exdw_lds_bytes(const ExDwArgs& a, int K);
+hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st);
 // sc_in != null: split output (f16 [hi32|lo32] groups, scale from split_a_exp)

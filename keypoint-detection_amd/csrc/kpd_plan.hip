@@ -9,6 +9,7 @@
 //   select_top_k_channels          dll/models/keypoint_model.py:90, 653-661
 //   per-box ROI / heatmap / decode dll/models/keypoint_model.py:143-199
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -108,6 +109,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* h3 = nullptr;
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
   float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
+  float* pool = nullptr;    // [B][1024] SE channel means from the fused expand+depthwise kernel
   float* sc = nullptr;    // split FPN scale inputs: slotted max|tap0|, max|lateral1| (amax_publish)
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
@@ -371,6 +373,7 @@ int pack_split16(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
 
 // ------------------------------------------------------------------ workspace
 constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
+constexpr int kFuseMaxPix = 16 * 12;        // input maps up to this size take the fused expand+depthwise
 
 struct Carver {
   char* base;
@@ -404,6 +407,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
   w.sc = c.take<float>(2 * kAmaxSlots * kAmaxStride);
   w.splitk = c.take<float>(kSplitKFloats);
+  w.pool = c.take<float>((size_t)B * 1024);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
@@ -792,16 +796,35 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     const DevBneck& bn = p->bn[i];
     const int hi = d.h[i], wi = d.w[i], ho = d.h[i + 1], wo = d.w[i + 1];
     const int inp = pad16(bn.cfg.cin);
-    const float* e = x;
-    if (bn.has_exp) {
-      if (int rc = conv(bn.expand, x, B, hi, wi, inp, w.e[i], bn.cfg.act, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-        return rc;
-      e = w.e[i];
+    // coarse maps: expand + depthwise (+ SE means) fused when the image fits LDS
+    ExDwArgs xa{};
+    xa.x = x; xa.Hi = hi; xa.Wi = wi; xa.cin_p = inp;
+    xa.we = bn.has_exp ? static_cast<const float*>(bn.expand.w) : nullptr;
+    xa.be = bn.has_exp ? bn.expand.b : nullptr;
+    xa.act_e = bn.cfg.act; xa.wd = bn.dw.w; xa.bd = bn.dw.b; xa.act_d = bn.dw.act; xa.Ep = bn.dw.Cp;
+    xa.out = w.d[i]; xa.Ho = ho; xa.Wo = wo; xa.pooled = bn.cfg.se ? w.pool : nullptr;
+    bool fused = false;
+    static const bool no_fuse = getenv("KPD_NO_FUSE") != nullptr;   // A/B switch for measurements
+    if (!no_fuse && hi * wi <= kFuseMaxPix && (!bn.has_exp || bn.expand.cout_p == bn.dw.Cp)) {
+      for (int cs : {16, 32, 48}) {   // narrow slices: more workgroups for these small layers
+        xa.CS = cs;
+        if (bn.dw.Cp % cs == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 64 * 1024) { fused = true; break; }
+      }
     }
-    HIP_TRY(launch_dwconv(e, bn.dw.w, bn.dw.b, w.d[i], B, hi, wi, bn.dw.Cp, ho, wo, bn.dw.k, bn.dw.s, bn.dw.act, st));
+    if (fused) {
+      HIP_TRY(launch_exdw(xa, B, bn.dw.k, bn.dw.s, st));
+    } else {
+      const float* e = x;
+      if (bn.has_exp) {
+        if (int rc = conv(bn.expand, x, B, hi, wi, inp, w.e[i], bn.cfg.act, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+          return rc;
+        e = w.e[i];
+      }
+      HIP_TRY(launch_dwconv(e, bn.dw.w, bn.dw.b, w.d[i], B, hi, wi, bn.dw.Cp, ho, wo, bn.dw.k, bn.dw.s, bn.dw.act, st));
+    }
     if (bn.cfg.se)
       HIP_TRY(launch_se(w.d[i], B, ho * wo, bn.se.C, bn.se.Cp, bn.se.w1, bn.se.b1, bn.se.w2, bn.se.b2, bn.se.sq,
-                        w.sesc[i], st));
+                        w.sesc[i], st, fused ? w.pool : nullptr));
     const bool res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
     if (int rc = conv(bn.project, w.d[i], B, ho, wo, bn.dw.Cp, w.o[i], ACT_NONE, res ? x : nullptr, ho, wo,
                       bn.cfg.se ? w.sesc[i] : nullptr, nullptr, 0, 0, st))

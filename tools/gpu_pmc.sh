@@ -15,6 +15,6 @@ i=0
 for G in "${PGROUPS[@]}"; do
   i=$((i + 1))
   timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --pmc $G --kernel-trace --output-format csv -d "$OUTD/pass$i" -o run -- \
-    python3 "$ROOTD/bench.py" --steps 3 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUTD/pass$i.log" 2>&1 || exit $?
+    python3 "$ROOTD/bench.py" --steps 3 --warmup 2 --no-cpu-baseline --streams 1 ${BENCH_ARGS:-} > "$OUTD/pass$i.log" 2>&1 || exit $?
 done
 python3 "$ROOTD/tools/pmc_summary.py" "$OUTD" | tee "$OUTD/summary.txt"
