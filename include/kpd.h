@@ -115,6 +115,20 @@ int kpd_plan_timing_query(kpd_plan* plan, const char* stage, double* total_ms, i
 int kpd_nms(const float* boxes, const float* scores, int n, float iou_threshold, int max_output,
             int32_t* keep, int32_t* n_keep, void* stream);
 
+/* Preprocessing: the reference's ITransform
+ * (dll/data/transforms.py:9-113) on the device.  src: uint8 HWC image
+ * (C = 1 or 3, row pitch in bytes, device memory); dst: fp32 [C'][out_h][out_w]
+ * (device), C' = 1 with KPD_PRE_GRAY.  Stages in order: RGB->gray (cv2
+ * fixed point), CLAHE per plane (clip_limit, tiles_x x tiles_y), Gaussian
+ * 3x3 sigma 0.5, PIL-exact bilinear resize, ToTensor + Normalize(mean, std)
+ * (host arrays of C' floats).  Stream-ordered scratch (hipMallocAsync). */
+#define KPD_PRE_GRAY 1
+#define KPD_PRE_CLAHE 2
+#define KPD_PRE_BLUR 4
+int kpd_preprocess(const uint8_t* src, int height, int width, int channels, int pitch, int flags, float clip_limit,
+                   int tiles_x, int tiles_y, int out_h, int out_w, const float* mean, const float* std, float* dst,
+                   void* stream);
+
 /* Concurrency: a forward pass over B >= 32 images runs as min(n, B/16)
  * contiguous sub-batches on as many streams (forked from / joined back into
  * the caller's stream), so the latency-bound small launches of one sub-batch

@@ -241,7 +241,6 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
   e.M = M; e.H = H; e.W = W; e.cout_p = cout_p; e.out_cstride = p.out_cstride; e.rh = p.rh; e.rw = p.rw;
   e.act = p.act; e.tiles_per_img = p.tiles_per_img;
   e.post_scale = p.post_scale; e.post_shift = p.post_shift; e.act2 = p.act2; e.act3 = p.act3;
-#pragma unroll
   for (int h = 0; h < HALVES; ++h) {
     if (h) __syncthreads();
     if constexpr (HALVES == 1) acc_to_lds<FM, FN, WM, WN, BN>(tile, acc, wm, wn, lane);

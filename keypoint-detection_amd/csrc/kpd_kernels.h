@@ -125,3 +125,7 @@ hipError_t launch_kh_final(const float* lin_r, int r_stride, const float* lin_v,
                            const float* ln_rb, const float* w_r, const float* b_r, const float* ln_vg,
                            const float* ln_vb, const float* w_v, const float* b_v, const int32_t* slot, int R, int P,
                            float* kh_kpts, float* kh_vis, hipStream_t st);
+
+// error reporting shared with the C ABI entry points outside kpd_plan.hip
+int kpd_fail_einval(const char* msg);
+int kpd_fail_hip(hipError_t e, const char* where);

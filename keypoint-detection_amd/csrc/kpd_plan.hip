@@ -39,6 +39,15 @@ int fail(int code, const std::string& msg) {
 
 inline int pad16(int c) { return (c + 15) / 16 * 16; }
 
+}  // namespace
+
+int kpd_fail_einval(const char* msg) { return fail(KPD_EINVAL, msg); }
+int kpd_fail_hip(hipError_t e, const char* where) {
+  return fail(KPD_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+namespace {
+
 struct HostT {
   std::vector<int64_t> shape;
   std::vector<float> data;

@@ -23,7 +23,7 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "mixed": KPD_PRECISION_MIXED, "bf16": 
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
            "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector", "kpd_bench_conv16",
-           "kpd_plan_set_streams")
+           "kpd_plan_set_streams", "kpd_preprocess")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",

@@ -1,0 +1,99 @@
+"""Preprocessing path: the oracle against real-Pillow
+golden vectors (CPU), and the HIP kernels (kpd_preprocess) against the golden
+vectors and the oracle (GPU).
+
+Tolerances: resize + ToTensor + Normalize bit-exact (uint8 fixed point and the
+same fp32 ops as torchvision); CLAHE, gray conversion and blur bit-exact vs the
+oracle restatement (parity unpinned vs OpenCV, which is absent).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import preprocess_oracle as O
+
+
+def _golden(golden_dir):
+    return np.load(golden_dir / "preprocess.npz", allow_pickle=False)
+
+
+def test_oracle_resize_matches_pillow(golden_dir):
+    g = _golden(golden_dir)
+    for i in range(int(g["n"])):
+        h, w, c, oh, ow = (int(v) for v in g[f"shape{i}"])
+        r = O.pil_resize_bilinear(g[f"img{i}"], oh, ow)
+        assert np.array_equal(r, g[f"resized{i}"]), i
+        if f"norm{i}" in g:
+            mean, std = ([0.485, 0.456, 0.406], [0.229, 0.224, 0.225]) if c == 3 else ([0.5], [0.5])
+            assert np.array_equal(O.to_tensor_normalize(r, mean, std), g[f"norm{i}"]), i
+
+
+def test_oracle_clahe_properties():
+    rng = np.random.default_rng(7)
+    flat = np.full((64, 48), 77, np.uint8)
+    out = O.clahe_u8(flat, 2.0, 8, 8)
+    assert (out == out[0, 0]).all()                       # a constant image stays constant
+    img = rng.integers(0, 256, (50, 70), dtype=np.uint8)  # ragged: reflect-101 padding path
+    a = O.clahe_u8(img, 2.0, 8, 8)
+    b = O.clahe_u8(img, 2.0, 8, 8)
+    assert np.array_equal(a, b) and a.shape == img.shape
+    # monotone per tile centre: within one tile LUT, larger input never maps lower
+    ramp = np.tile(np.arange(256, dtype=np.uint8), (16, 1))
+    r = O.clahe_u8(ramp, 40.0, 1, 1)
+    assert (np.diff(r[8].astype(int)) >= 0).all()
+
+
+def test_itransform_api_importable():
+    from dll.data import ITransform
+    t = ITransform(img_size=64, clip_limit=2.0, tile_size=(8, 8), grayscale=False, device="cpu")
+    assert t.size == (64, 64) and t.grayscale is False
+
+
+gpu = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@gpu
+def test_gpu_resize_normalize_vs_pillow(golden_dir):
+    from dll.data.transforms import preprocess
+    g = _golden(golden_dir)
+    for i in range(int(g["n"])):
+        h, w, c, oh, ow = (int(v) for v in g[f"shape{i}"])
+        img = torch.from_numpy(g[f"img{i}"]).to(DEV)
+        mean, std = ([0.485, 0.456, 0.406], [0.229, 0.224, 0.225]) if c == 3 else ([0.5], [0.5])
+        out = preprocess(img, (oh, ow), mean, std).cpu().numpy()
+        want = O.to_tensor_normalize(g[f"resized{i}"], mean, std)
+        assert np.array_equal(out, want), i
+        if f"norm{i}" in g:
+            assert np.array_equal(out, g[f"norm{i}"]), i
+
+
+@gpu
+def test_gpu_clahe_gray_blur_vs_oracle():
+    from dll.data.transforms import FLAG_BLUR, FLAG_CLAHE, FLAG_GRAY, preprocess
+    rng = np.random.default_rng(11)
+    for (h, w) in ((96, 128), (101, 77)):                 # tile multiple and ragged (reflect-101)
+        yy, xx = np.mgrid[0:h, 0:w]
+        img = ((rng.integers(0, 80, (h, w, 3)) + ((yy * 2 + xx)[..., None] % 176)) % 256).astype(np.uint8)
+        t = torch.from_numpy(img).to(DEV)
+        # gray + CLAHE, no resize
+        got = preprocess(t, (h, w), [0.0], [1.0 / 255.0], FLAG_GRAY | FLAG_CLAHE, 2.0, (8, 8)).cpu().numpy()[0]
+        want = O.clahe_u8(O.rgb_to_gray_cv(img), 2.0, 8, 8).astype(np.float32)
+        assert np.array_equal(np.rint(got).astype(np.int64), want.astype(np.int64))
+        # RGB ITransform pipeline: CLAHE per channel + blur + resize + normalise
+        got = preprocess(t, (64, 64), [0.485, 0.456, 0.406], [0.229, 0.224, 0.225], FLAG_CLAHE | FLAG_BLUR, 2.0,
+                         (8, 8)).cpu().numpy()
+        want = O.itransform_rgb(img, 64, 2.0, (8, 8))
+        assert np.array_equal(got, want)
+
+
+@gpu
+def test_gpu_itransform_dropin_matches_oracle():
+    from PIL import Image
+    from dll.data import ITransform
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (120, 90, 3), dtype=np.uint8)
+    t = ITransform(img_size=96, clip_limit=2.0, tile_size=(8, 8), grayscale=False, device=DEV)
+    out = t(Image.fromarray(img)).cpu().numpy()
+    assert out.shape == (3, 96, 96)
+    assert np.array_equal(out, O.itransform_rgb(img, 96, 2.0, (8, 8)))
