@@ -119,12 +119,16 @@ int kpd_nms(const float* boxes, const float* scores, int n, float iou_threshold,
  * (dll/data/transforms.py:9-113) on the device.  src: uint8 HWC image
  * (C = 1 or 3, row pitch in bytes, device memory); dst: fp32 [C'][out_h][out_w]
  * (device), C' = 1 with KPD_PRE_GRAY.  Stages in order: RGB->gray (cv2
- * fixed point), CLAHE per plane (clip_limit, tiles_x x tiles_y), Gaussian
- * 3x3 sigma 0.5, PIL-exact bilinear resize, ToTensor + Normalize(mean, std)
- * (host arrays of C' floats).  Stream-ordered scratch (hipMallocAsync). */
+ * fixed point), CLAHE per plane (clip_limit, tiles_x x tiles_y), the gray
+ * pipeline's edge blend (to_grayscale_clahe :55-73: blur, median, Canny,
+ * morphology, addWeighted; single plane only), Gaussian 3x3 sigma 0.5 (RGB
+ * pipeline, :105), PIL-exact bilinear resize, ToTensor + Normalize(mean, std)
+ * (host arrays of C' floats).  Stream-ordered scratch (hipMallocAsync).
+ * Replaces ITransform.__call__ (transforms.py:110-113). */
 #define KPD_PRE_GRAY 1
 #define KPD_PRE_CLAHE 2
 #define KPD_PRE_BLUR 4
+#define KPD_PRE_EDGES 8
 int kpd_preprocess(const uint8_t* src, int height, int width, int channels, int pitch, int flags, float clip_limit,
                    int tiles_x, int tiles_y, int out_h, int out_w, const float* mean, const float* std, float* dst,
                    void* stream);

@@ -6,15 +6,16 @@ Reference pipeline and what runs here:
 * RGB (``grayscale=False``, :36-41, :80-108): per-channel CLAHE -> 3x3
   Gaussian (sigma 0.5) -> Resize((s, s)) -> ToTensor -> Normalize(ImageNet).
   All stages run on the device.
-* Grayscale (``grayscale=True``, :28-33, :43-78): RGB->gray -> CLAHE -> Canny
-  edge blend -> Resize -> ToTensor -> Normalize(0.5, 0.5).  The gray
-  conversion, CLAHE, resize and normalisation run on the device; the Canny /
-  morphology edge blend is not implemented yet, so this mode
-  returns the CLAHE image without the 0.3-weighted edge map.
+* Grayscale (``grayscale=True``, :28-33, :43-78): RGB->gray -> CLAHE -> edge
+  blend (GaussianBlur 5x5 -> medianBlur 5 -> Canny(100, 200) -> dilate/erode
+  x2 -> GaussianBlur 3x3 -> scale to 255 -> addWeighted(0.7, 0.3)) -> Resize
+  -> ToTensor -> Normalize(0.5, 0.5).  All stages run on the device.
 
 Resize/ToTensor/Normalize are bit-exact to Pillow + torchvision
-(tests/golden/preprocess.npz).  CLAHE and the blur restate OpenCV's algorithms
-(parity unpinned: OpenCV is not available to compare against).
+(tests/golden/preprocess.npz).  CLAHE, the blurs, median, Canny, morphology
+and addWeighted restate OpenCV's CV_8U algorithms and are bit-exact to the
+oracle (oracle/preprocess_oracle.py) -- parity unpinned against OpenCV itself,
+which is absent from this image.
 """
 import ctypes
 from typing import Optional, Sequence, Tuple, Union
@@ -24,7 +25,7 @@ import torch
 
 from .. import _native
 
-FLAG_GRAY, FLAG_CLAHE, FLAG_BLUR = 1, 2, 4
+FLAG_GRAY, FLAG_CLAHE, FLAG_BLUR, FLAG_EDGES = 1, 2, 4, 8
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
@@ -80,7 +81,7 @@ class ITransform:
             raise TypeError("ITransform expects 8-bit images")
         t = t.to(self.device, non_blocking=True)
         if self.grayscale:
-            flags = FLAG_CLAHE | (FLAG_GRAY if t.dim() == 3 and t.shape[2] == 3 else 0)
+            flags = FLAG_CLAHE | FLAG_EDGES | (FLAG_GRAY if t.dim() == 3 and t.shape[2] == 3 else 0)
             return preprocess(t, self.size, (0.5,), (0.5,), flags, self.clip_limit, self.tile_size)
         if t.dim() == 2:
             t = t[:, :, None].expand(-1, -1, 3)

@@ -6,9 +6,9 @@
         --model best_model.pth --input img.jpg --gt img.txt --output out/
 
 Differences (documented in DESIGN.md):
-  * the reference's ITransform needs OpenCV (CLAHE + Canny blend), absent in
-    this image; the image is resized/normalised like ITransform's torchvision
-    tail (Resize, ToTensor, Normalize) without the cv2 stage;
+  * ITransform runs on the device (dll.data.ITransform): its OpenCV stages
+    (CLAHE, Canny edge blend, blur) are restated in HIP, since OpenCV is absent
+    in this image; Resize/ToTensor/Normalize are bit-exact to Pillow;
   * ``--model synthetic`` builds the seeded synthetic weights (no trained
     checkpoint exists: the reference's outputs/best_model.pth is a missing blob);
   * ``--size HxW`` allows the non-square 256x192 input of BASELINE config C1.
@@ -27,6 +27,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 from dll.configs import (BackboneConfig, KeypointHeadConfig, ModelConfig,  # noqa: E402
                          PersonDetectionConfig, TrainingConfig)
+from dll.data import ITransform  # noqa: E402
 from dll.models import MultiPersonKeypointModel  # noqa: E402
 
 KEYPOINT_NAMES = ["nose", "left_eye", "right_eye", "left_ear", "right_ear", "left_shoulder", "right_shoulder",
@@ -65,21 +66,12 @@ def load_model(model_path, config_dict, device, precision="fp32"):
     return model.to(device).eval()
 
 
-def make_transform(in_channels: int, size):
-    """Resize -> ToTensor -> Normalize (ITransform without its cv2 stage)."""
-    h, w = size
-
-    def tf(img):
-        import numpy as np
-        img = img.convert("L" if in_channels == 1 else "RGB").resize((w, h), resample=2)  # bilinear
-        x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0)
-        x = x[None] if x.dim() == 2 else x.permute(2, 0, 1)
-        if in_channels == 1:
-            return (x - 0.5) / 0.5
-        m = torch.tensor([0.485, 0.456, 0.406]).view(3, 1, 1)
-        s = torch.tensor([0.229, 0.224, 0.225]).view(3, 1, 1)
-        return (x - m) / s
-    return tf
+def make_transform(in_channels: int, size, device):
+    """The reference's ITransform(img_size, clip_limit=2.0, tile_size=(8, 8))
+    (predict.py:179-183) on the device (dll.data.ITransform, kpd_preprocess):
+    the grayscale pipeline (CLAHE + edge blend) for a 1-channel backbone, the
+    RGB pipeline for a 3-channel one."""
+    return ITransform(img_size=size, clip_limit=2.0, tile_size=(8, 8), grayscale=(in_channels == 1), device=device)
 
 
 def read_gt_boxes(gt_path, device):
@@ -95,7 +87,7 @@ def read_gt_boxes(gt_path, device):
 
 def predict_single_image(model, image_path, transform, device, gt_path=None, output_path=None):
     from PIL import Image
-    x = transform(Image.open(image_path)).unsqueeze(0).to(device)
+    x = transform(Image.open(image_path).convert("RGB")).unsqueeze(0).to(device)
     bboxes = read_gt_boxes(gt_path, device) if gt_path and Path(gt_path).exists() else None
     with torch.no_grad():
         outputs = model({"image": x, "bboxes": bboxes.unsqueeze(0) if bboxes is not None else None})
@@ -128,7 +120,7 @@ def main(argv=None):
     device = torch.device(args.device)
     bcfg = cfg["model"]["backbone"]
     size = tuple(int(v) for v in args.size.split("x")) if args.size else (bcfg["input_size"], bcfg["input_size"])
-    transform = make_transform(bcfg.get("in_channels", 3), size)
+    transform = make_transform(bcfg.get("in_channels", 3), size, device)
     logging.info(f"Loading model from {args.model}")
     model = load_model(args.model, cfg, device, args.precision)
     inp = Path(args.input)

@@ -20,9 +20,14 @@ Reference: `ITransform` (dll/data/transforms.py:9-113) = an OpenCV stage
   LUT = saturate_cast<uchar>(cumsum * 255 / area), bilinear blend of the four
   neighbouring tile LUTs).  OpenCV is absent from this image and from the GPU
   box, so this restatement is **parity unpinned** against OpenCV itself.
-* `gaussian_blur3_u8` (the RGB pipeline's `GaussianBlur((3, 3), 0.5)`) is a
-  float separable restatement, also **parity unpinned** (OpenCV's 8-bit
-  fixed-point path may differ by one grey level at rounding ties).
+* `gaussian_blur_u8` restates cv::GaussianBlur's CV_8U fixed-point path
+  (getGaussianKernelBitExact -> 8-bit error-diffused kernel, exact integer
+  row/column sums, round half up); `median5_u8`, `canny_u8` (L1, aperture 3),
+  `morph3_u8` and `add_weighted_u8` restate medianBlur / Canny / dilate /
+  erode / addWeighted for the grayscale pipeline's edge blend
+  (`edge_blend_u8`, transforms.py:55-73).  All **parity unpinned** against
+  OpenCV (absent); median, morphology and Canny are integer algorithms whose
+  only freedom is the documented border and tie rules.
 """
 import numpy as np
 
@@ -189,34 +194,162 @@ def clahe_u8(img: np.ndarray, clip_limit: float, tiles_x: int, tiles_y: int) -> 
     return out
 
 
-def gaussian_kernel(ksize: int, sigma: float) -> np.ndarray:
-    """cv::getGaussianKernel (sigma > 0): exp(-(i - c)^2 / (2 sigma^2)), normalised."""
-    c = (ksize - 1) / 2.0
-    k = [float(np.exp(-((i - c) ** 2) / (2.0 * sigma * sigma))) for i in range(ksize)]
-    s = 0.0
-    for v in k:          # accumulated in index order, as getGaussianKernel does
-        s += v
-    return np.array([v / s for v in k])
+def gaussian_kernel_bitexact(ksize: int, sigma: float) -> np.ndarray:
+    """cv::getGaussianKernelBitExact (imgproc/src/smooth.dispatch.cpp): the
+    fixed table for sigma <= 0 and ksize <= 7, else exp(x^2 * (-0.125 / s^2))
+    over doubled coordinates x = 2i - (n - 1), normalised by 1 / sum with the
+    centre tap exactly 1 * mul1."""
+    n = ksize
+    if sigma <= 0 and n in (1, 3, 5, 7):
+        return np.array({1: [1.0], 3: [0.25, 0.5, 0.25], 5: [0.0625, 0.25, 0.375, 0.25, 0.0625],
+                         7: [0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125]}[n])
+    sig = sigma if sigma > 0 else n * 0.15 + 0.35
+    scale2x = -0.125 / (sig * sig)
+    n2 = (n - 1) // 2
+    values, s = [], 0.0
+    for i in range(n2):
+        x = 2 * i + 1 - n
+        t = float(np.exp(float(x * x) * scale2x))
+        values.append(t)
+        s += t
+    s = s * 2.0 + 1.0
+    mul1 = 1.0 / s
+    r = np.zeros(n)
+    for i in range(n2):
+        r[i] = r[n - 1 - i] = values[i] * mul1
+    r[n2] = mul1
+    return r
 
 
-def gaussian_blur3_u8(img: np.ndarray, sigma: float) -> np.ndarray:
-    """Separable 3x3 Gaussian on uint8 planes, reflect-101 border, fp32 with
-    round-half-even to uint8 (parity unpinned vs OpenCV's fixed-point path)."""
-    k = gaussian_kernel(3, sigma).astype(np.float32)
+def gaussian_kernel_fixed(ksize: int, sigma: float) -> np.ndarray:
+    """getGaussianKernelFixedPoint_ED with 8 fraction bits (ufixedpoint16, the
+    type cv::GaussianBlur uses for CV_8U): error-diffused cvRound of the outer
+    taps, centre = 256 - sum of the others."""
+    k = gaussian_kernel_bitexact(ksize, sigma)
+    n2 = ksize // 2
+    out = np.zeros(ksize, np.int64)
+    err, s = 0.0, 0
+    for i in range(n2):
+        adj = k[i] * 256.0 + err
+        v0 = int(np.rint(adj))            # cvRound: half to even
+        err = adj - v0
+        out[i] = out[ksize - 1 - i] = v0
+        s += v0
+    out[n2] = 256 - 2 * s
+    return out
+
+
+def gaussian_blur_u8(img: np.ndarray, ksize: int, sigma: float) -> np.ndarray:
+    """cv::GaussianBlur on CV_8U via the fixed-point path (GaussianBlurFixedPoint):
+    reflect-101 border; the row pass is the exact integer sum of kernel(8-bit
+    fraction) x pixel, the column pass the exact sum of kernel x row value
+    (16-bit fraction), rounded half up to uint8."""
+    k = gaussian_kernel_fixed(ksize, sigma)
     a = img if img.ndim == 3 else img[:, :, None]
     H, W, C = a.shape
-    ys = [np.array([_reflect101(y + d, H) for y in range(H)]) for d in (-1, 0, 1)]
-    xs = [np.array([_reflect101(x + d, W) for x in range(W)]) for d in (-1, 0, 1)]
-    f = a.astype(np.float32)
-    h = k[0] * f[:, xs[0]] + k[1] * f[:, xs[1]] + k[2] * f[:, xs[2]]
-    v = k[0] * h[ys[0]] + k[1] * h[ys[1]] + k[2] * h[ys[2]]
-    out = np.clip(np.rint(v), 0, 255).astype(np.uint8)
+    r = ksize // 2
+    ys = [np.array([_reflect101(y + d, H) for y in range(H)]) for d in range(-r, r + 1)]
+    xs = [np.array([_reflect101(x + d, W) for x in range(W)]) for d in range(-r, r + 1)]
+    f = a.astype(np.int64)
+    h = sum(k[i] * f[:, xs[i]] for i in range(ksize))
+    v = sum(k[i] * h[ys[i]] for i in range(ksize))
+    out = np.minimum((v + (1 << 15)) >> 16, 255).astype(np.uint8)
     return out if img.ndim == 3 else out[:, :, 0]
+
+
+def median5_u8(img: np.ndarray) -> np.ndarray:
+    """cv::medianBlur(img, 5) for CV_8U (the sorting-network path, replicated border)."""
+    p = np.pad(img, 2, mode="edge")
+    win = np.lib.stride_tricks.sliding_window_view(p, (5, 5)).reshape(img.shape[0], img.shape[1], 25)
+    return np.sort(win, axis=-1)[..., 12].astype(np.uint8)
+
+
+CANNY_TG22 = int(0.4142135623730950488016887242097 * (1 << 15) + 0.5)
+
+
+def canny_u8(img: np.ndarray, low: float, high: float) -> np.ndarray:
+    """cv::Canny(img, low, high) with apertureSize 3 and the L1 gradient
+    (imgproc/src/canny.cpp): 3x3 Sobel (replicated border) in int, magnitude
+    |dx| + |dy| (zero outside the image), non-maximum suppression by the
+    tan(22.5)/tan(67.5) fixed-point sector test (strict '>' toward the
+    previous neighbour, '>=' toward the next; both strict on diagonals),
+    candidates m > floor(low), seeds m > floor(high), 8-connected hysteresis.
+    Returns 0/255."""
+    lo, hi = int(np.floor(low)), int(np.floor(high))
+    p = np.pad(img.astype(np.int64), 1, mode="edge")
+    dx = (p[:-2, 2:] + 2 * p[1:-1, 2:] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[1:-1, :-2] + p[2:, :-2])
+    dy = (p[2:, :-2] + 2 * p[2:, 1:-1] + p[2:, 2:]) - (p[:-2, :-2] + 2 * p[:-2, 1:-1] + p[:-2, 2:])
+    mag = np.abs(dx) + np.abs(dy)
+    M = np.pad(mag, 1)
+    ax, ay = np.abs(dx), np.abs(dy) << 15
+    tg22x = ax * CANNY_TG22
+    tg67x = tg22x + (ax << 16)
+    horiz = ay < tg22x
+    vert = ~horiz & (ay > tg67x)
+    diag = ~horiz & ~vert
+    neg = (dx ^ dy) < 0
+    c = M[1:-1, 1:-1]
+    keep_h = (c > M[1:-1, :-2]) & (c >= M[1:-1, 2:])
+    keep_v = (c > M[:-2, 1:-1]) & (c >= M[2:, 1:-1])
+    keep_d = np.where(neg, (c > M[:-2, 2:]) & (c > M[2:, :-2]),      # s = -1: (y-1, x+1) and (y+1, x-1)
+                      (c > M[:-2, :-2]) & (c > M[2:, 2:]))            # s = +1: (y-1, x-1) and (y+1, x+1)
+    nms = (horiz & keep_h) | (vert & keep_v) | (diag & keep_d)
+    cand = (mag > lo) & nms
+    strong = cand & (mag > hi)
+    from scipy import ndimage
+    lab, nlab = ndimage.label(cand, structure=np.ones((3, 3), int))
+    seeded = np.zeros(nlab + 1, bool)
+    seeded[np.unique(lab[strong])] = True
+    seeded[0] = False
+    return np.where(seeded[lab], 255, 0).astype(np.uint8)
+
+
+def morph3_u8(img: np.ndarray, dilate: bool) -> np.ndarray:
+    """cv::dilate / cv::erode with np.ones((3, 3)), one iteration, default
+    border (the out-of-image value never wins)."""
+    p = np.pad(img, 1, constant_values=0 if dilate else 255)
+    win = np.lib.stride_tricks.sliding_window_view(p, (3, 3))
+    return (win.max(axis=(-1, -2)) if dilate else win.min(axis=(-1, -2))).astype(np.uint8)
+
+
+def add_weighted_u8(a: np.ndarray, alpha: float, b: np.ndarray, beta: float) -> np.ndarray:
+    """cv::addWeighted for CV_8U, gamma 0: fp32 fma(a, alpha, fma(b, beta, 0))
+    (the SIMD path), cvRound half to even, saturate.  Evaluated in double,
+    where both products and the sum are exact, then rounded once to fp32 --
+    the same value the fused multiply-adds give."""
+    al, be = float(np.float32(alpha)), float(np.float32(beta))
+    inner = (b.astype(np.float64) * be).astype(np.float32).astype(np.float64)
+    t = (a.astype(np.float64) * al + inner).astype(np.float32)
+    return np.clip(np.rint(t), 0, 255).astype(np.uint8)
+
+
+def edge_blend_u8(clahe_img: np.ndarray) -> np.ndarray:
+    """The edge half of to_grayscale_clahe (transforms.py:55-73):
+    GaussianBlur 5x5 s1.5 -> medianBlur 5 -> Canny(100, 200) -> (dilate,
+    erode) x 2 with a 3x3 ones kernel -> GaussianBlur 3x3 s0 -> scale to max
+    255 (float64, truncating astype) -> addWeighted(clahe 0.7, edges 0.3)."""
+    d = median5_u8(gaussian_blur_u8(clahe_img, 5, 1.5))
+    e = canny_u8(d, 100, 200)
+    e = morph3_u8(morph3_u8(morph3_u8(morph3_u8(e, True), False), True), False)
+    e = gaussian_blur_u8(e, 3, 0)
+    mx = int(e.max())
+    if mx > 0:
+        e = (e.astype(np.float64) / mx * 255).astype(np.uint8)
+    return add_weighted_u8(clahe_img, 0.7, e, 0.3)
+
+
+def itransform_gray(img: np.ndarray, size, clip_limit: float = 1.5, tiles=(8, 8)) -> np.ndarray:
+    """ITransform(grayscale=True) (transforms.py:28-33,43-78) -> fp32 [1,h,w]."""
+    oh, ow = (size, size) if isinstance(size, int) else size
+    gray = img if img.ndim == 2 else rgb_to_gray_cv(img)
+    x = edge_blend_u8(clahe_u8(np.ascontiguousarray(gray), clip_limit, tiles[0], tiles[1]))
+    x = pil_resize_bilinear(x, oh, ow)
+    return to_tensor_normalize(x, [0.5], [0.5])
 
 
 def itransform_rgb(img: np.ndarray, size: int, clip_limit: float = 2.0, tiles=(8, 8)) -> np.ndarray:
     """ITransform(grayscale=False) (transforms.py:36-41,80-108) -> fp32 [3,s,s]."""
     planes = [clahe_u8(np.ascontiguousarray(img[..., c]), clip_limit, tiles[0], tiles[1]) for c in range(3)]
-    x = gaussian_blur3_u8(np.stack(planes, -1), 0.5)
+    x = gaussian_blur_u8(np.stack(planes, -1), 3, 0.5)
     x = pil_resize_bilinear(x, size, size)
     return to_tensor_normalize(x, [0.485, 0.456, 0.406], [0.229, 0.224, 0.225])
