@@ -133,6 +133,22 @@ int kpd_preprocess(const uint8_t* src, int height, int width, int channels, int 
                    int tiles_x, int tiles_y, int out_h, int out_w, const float* mean, const float* std, float* dst,
                    void* stream);
 
+/* Training / evaluation targets: generate_target_heatmap
+ * (dll/models/heatmap_head.py:163-224).  kpts: [planes][2] normalised (x, y)
+ * (device), out: [planes][H][W] fp32 (device); the (6*int(sigma)+1)^2
+ * normalised Gaussian is centred at (floor(x*W), floor(y*H)) and cropped;
+ * keypoints outside [0,1) leave their plane zero.  Synchronises the stream
+ * (the kernel table is staged from host memory). */
+int kpd_target_heatmaps(const float* kpts, int planes, int H, int W, float sigma, float* out, void* stream);
+
+/* Validation metrics: Trainer._calculate_validation_metrics
+ * (dll/training/trainer.py:384-429).  pred, gt: [n][2], vis: [n] (device);
+ * thresholds: host array (<= 16).  out (device) = [ADE, PCK_t...]: ADE = mean
+ * ||pred-gt|| over vis > 0, PCK_t = #(dist <= t and vis > 0) / n; all zero
+ * when nothing is visible. */
+int kpd_keypoint_metrics(const float* pred, const float* gt, const float* vis, long n, const float* thresholds,
+                         int n_thresholds, float* out, void* stream);
+
 /* Concurrency: a forward pass over B >= 32 images runs as min(n, B/16)
  * contiguous sub-batches on as many streams (forked from / joined back into
  * the caller's stream), so the latency-bound small launches of one sub-batch

@@ -23,7 +23,7 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "mixed": KPD_PRECISION_MIXED, "bf16": 
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
            "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector", "kpd_bench_conv16",
-           "kpd_plan_set_streams", "kpd_preprocess")
+           "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",
@@ -63,6 +63,9 @@ def load() -> ctypes.CDLL:
     lib.kpd_plan_timing.argtypes = [c_void_p, c_int]
     lib.kpd_plan_timing_query.argtypes = [c_void_p, c_char_p, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(c_int)]
+    lib.kpd_target_heatmaps.argtypes = [c_void_p, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]
+    lib.kpd_keypoint_metrics.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_float),
+                                         c_int, c_void_p, c_void_p]
     lib.kpd_nms.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_float, c_int, c_void_p, c_void_p, c_void_p]
     for name in EXPORTS:
         if name not in ("kpd_last_error", "kpd_version", "kpd_plan_destroy"):

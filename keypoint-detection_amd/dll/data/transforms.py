@@ -69,6 +69,7 @@ class ITransform:
         self.tile_size = tile_size
         self.grayscale = grayscale
         self.device = torch.device(device)
+        self.transform = self.__call__      # the reference's Compose pipeline attribute (:26-41)
 
     def __call__(self, img) -> torch.Tensor:
         if isinstance(img, torch.Tensor):

@@ -7,8 +7,13 @@ Same submodule names as the reference -- ``channel_attention.fc.{0,2}``,
 native plan for all ROIs of a batch at once (csrc/head_kernels.hip,
 csrc/conv_mfma.hip).
 """
+import ctypes
+from typing import Tuple
+
+import torch
 import torch.nn as nn
 
+from .. import _native
 from ..configs.model_config import HeatmapHeadConfig
 
 
@@ -52,3 +57,36 @@ class HeatmapHead(nn.Module):
             elif isinstance(m, nn.BatchNorm2d):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
+
+
+def generate_target_heatmap(keypoints: torch.Tensor, heatmap_size: Tuple[int, int], sigma: float = 3.0) -> torch.Tensor:
+    """Gaussian training targets (reference heatmap_head.py:163-224) on the
+    device (``kpd_target_heatmaps``).  [B,P,K,2] input is flattened to B*P
+    rows of which the reference fills the first B (its loop runs over B);
+    [B,K,2] gives one plane set per row.  Returns [B,K,H,W] fp32.  Values
+    match the reference within fp32 rounding of the normalised kernel."""
+    if keypoints.dim() == 4:
+        B, P, K, _ = keypoints.shape
+        kp = keypoints.reshape(B * P, K, -1)[:B]
+    elif keypoints.dim() == 3:
+        B, K, _ = keypoints.shape
+        kp = keypoints
+    else:
+        raise ValueError(f"Unexpected keypoints shape: {keypoints.shape}")
+    _native._require_cuda(keypoints, "keypoints")
+    H, W = int(heatmap_size[0]), int(heatmap_size[1])
+    kp = kp[..., :2].float().contiguous()
+    out = torch.empty(B, K, H, W, device=kp.device, dtype=torch.float32)
+    lib = _native.load()
+    with torch.cuda.device(kp.device):
+        rc = lib.kpd_target_heatmaps(_native._ptr(kp), B * K, H, W, ctypes.c_float(sigma), _native._ptr(out),
+                                     _native._stream(kp.device))
+    _native.check(rc, "kpd_target_heatmaps")
+    return out
+
+
+def generate_target_heatmap_adaptive(keypoints: torch.Tensor, heatmap_size: Tuple[int, int],
+                                     base_sigma: float = 3.0, adaptive: bool = True) -> torch.Tensor:
+    """Reference :226-252: sigma scaled with min(H, W) / 56, floored at 0.8x."""
+    sigma = base_sigma * max(0.8, min(heatmap_size) / 56.0) if adaptive else base_sigma
+    return generate_target_heatmap(keypoints, heatmap_size, sigma)
