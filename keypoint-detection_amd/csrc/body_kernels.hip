@@ -11,16 +11,22 @@
 //   * channel_stats: per-image channel sum/max partials for ChannelAttention
 //     when the FPN conv epilogue cannot produce them (H*W not a tile multiple).
 #include <algorithm>
+#include <cstdlib>
 
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 
 namespace {
 
-__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img, int N, int Cin, int H,
-                                                   int W, const float* __restrict__ w,
-                                                   const float* __restrict__ b, float* __restrict__ out,
-                                                   int Ho, int Wo, float* __restrict__ amax) {
+// Stem: 3x3 stride-2 conv (CIN -> 16) + folded BN + h-swish, NCHW image in,
+// NHWC out; CIN is a template argument so the 9*CIN inputs stay in registers.
+template <int CIN>
+__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img, int N, int H, int W,
+                                                   const float* __restrict__ w, const float* __restrict__ b,
+                                                   float* __restrict__ out, int Ho, int Wo,
+                                                   float* __restrict__ amax) {
+  constexpr int Cin = CIN;
+  __shared__ float4 so[256 * 4];
   __shared__ float sw[16 * 27];
   __shared__ float sb[16];
   __shared__ float red[4];
@@ -31,7 +37,8 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
   const int pix = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = pix < N * Ho * Wo;
   const int n = pix / (Ho * Wo), r = pix - n * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
-  float in[27];
+  float in[Cin * 9];
+#pragma unroll
   for (int c = 0; c < Cin; ++c)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
@@ -46,14 +53,25 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
 #pragma unroll
   for (int co = 0; co < 16; ++co) {
     float a = 0.f;
+#pragma unroll
     for (int k = 0; k < Cin * 9; ++k) a = fmaf(in[k], sw[co * Cin * 9 + k], a);
     o[co] = kpd_act(a + sb[co], ACT_HSWISH);
     m_abs = fmaxf(m_abs, fabsf(o[co]));
   }
-  if (live) {
-    float4* dst = reinterpret_cast<float4*>(out + (size_t)pix * 16);
+  // stage the block's 256 x 64-byte outputs in LDS (XOR-swizzled quads), then
+  // store them as one contiguous 16 KB run: each store instruction covers
+  // 1 KB of consecutive addresses instead of a 16-byte piece of every 64
+  const int t = threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  for (int q = 0; q < 4; ++q)
+    so[t * 4 + (q ^ (t & 3))] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  __syncthreads();
+  const int pix0 = blockIdx.x * blockDim.x, npx = min(256, N * Ho * Wo - pix0);
+  float4* dst = reinterpret_cast<float4*>(out + (size_t)pix0 * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = q * 256 + t, px = i >> 2, qq = i & 3;
+    if (px < npx) dst[i] = so[px * 4 + (qq ^ (px & 3))];
   }
   if (amax) {   // max|tap0| for the split FPN scale bound (conv_glds.hip)
     const float wm = wave_max(live ? m_abs : 0.f);
@@ -119,6 +137,79 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ i
     r.x = kpd_act(acc[o].x + bb.x, act); r.y = kpd_act(acc[o].y + bb.y, act);
     r.z = kpd_act(acc[o].z + bb.z, act); r.w = kpd_act(acc[o].w + bb.w, act);
     *reinterpret_cast<float4*>(op + (size_t)o * Cp) = r;
+  }
+}
+
+// SE excitation from the channel means (in LDS): fc1 + ReLU, fc2 +
+// hardsigmoid.  NT threads; the arithmetic order does not depend on NT (a
+// row of fc1 is one wave's reduction, an output of fc2 one thread's chain).
+// (A fused "last slice of the image runs the excitation" tail in exdw_kernel
+// was measured and dropped: the device-scope fence it needs writes back the
+// XCD's L2 and made the kernel 6x slower.)
+template <int NT, int IPW>
+__device__ __forceinline__ void se_fc(const float* mean, float* hid, int nimg, int C, int Cp,
+                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                      const float* __restrict__ w2t, const float* __restrict__ b2, int sq,
+                                      float* __restrict__ scale) {
+  // mean: [IPW][Cp] (LDS), hid: [IPW][256] (LDS), scale: [IPW][Cp] rows (global)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (2) fc1 + ReLU: wave per output row, lanes split K with 16-byte loads;
+  // up to 3 rows x 4 K-chunks (C <= 1024) issued before the reductions; each
+  // weight load serves the IPW images
+  const int nch = (C + 255) / 256;
+  for (int j0 = wave * 3; j0 < sq; j0 += (NT / 64) * 3) {
+    float acc[3][IPW];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int j = j0 + r;
+      if (j < sq) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int c = t * 256 + lane * 4;
+          if (t < nch && c < C) {
+            const float4 wv = *reinterpret_cast<const float4*>(w1 + (size_t)j * C + c);
+#pragma unroll
+            for (int m = 0; m < IPW; ++m) {
+              const float4 mv = *reinterpret_cast<const float4*>(mean + m * Cp + c);
+              acc[r][m] = fmaf(wv.x, mv.x, fmaf(wv.y, mv.y, fmaf(wv.z, mv.z, fmaf(wv.w, mv.w, acc[r][m]))));
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int m = 0; m < IPW; ++m) {
+        const float v = wave_sum(acc[r][m]);
+        if (lane == 0 && j0 + r < sq) hid[m * 256 + j0 + r] = fmaxf(v + b1[j0 + r], 0.f);
+      }
+  }
+  __syncthreads();
+  // (3) fc2 + hardsigmoid: thread per output over the transposed weights
+  // (coalesced rows), K unrolled with two accumulators per image
+  for (int c = tid; c < Cp; c += NT) {
+    float a0[IPW], a1[IPW];
+#pragma unroll
+    for (int m = 0; m < IPW; ++m) a0[m] = a1[m] = 0.f;
+    if (c < C) {
+#pragma unroll 4
+      for (int j = 0; j < sq; j += 2) {
+        const float wa = w2t[(size_t)j * C + c], wb = w2t[(size_t)(j + 1) * C + c];
+#pragma unroll
+        for (int m = 0; m < IPW; ++m) {
+          a0[m] = fmaf(wa, hid[m * 256 + j], a0[m]);
+          a1[m] = fmaf(wb, hid[m * 256 + j + 1], a1[m]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < IPW; ++m)
+      if (m < nimg) scale[(size_t)m * Cp + c] = c < C ? kpd_hsigmoid(a0[m] + a1[m] + b2[c]) : 0.f;
   }
 }
 
@@ -258,113 +349,88 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   }
 }
 
-// Squeeze-excitation, one 1024-thread workgroup (16 waves) per image: the
-// three steps are dependent, so each is laid out for memory-level parallelism
-// (all of a step's loads in flight together) rather than per-thread loops.
+// Squeeze-excitation, one 1024-thread workgroup (16 waves) per kSeImages
+// images (the fc weights are the bulk of the traffic, so each weight load
+// serves several images).  The three steps are dependent, so each is laid
+// out for memory-level parallelism (all of a step's loads in flight
+// together) rather than per-thread loops.
 //   x: [N][HW][Cp]; w1 = fc1 [sq][C] (row-major, as stored); w2t = fc2
 //   TRANSPOSED [sq][C]; scale out: [N][Cp] (hardsigmoid, 0 in padding).
 // torchvision SqueezeExcitation (backbone.py:250 via mobilenet_v3_small).
 constexpr int kSeThreads = 1024;
-__global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict__ x, int HW, int C, int Cp,
+constexpr int kSeImages = 1;   // images per workgroup (4 was measured slower: 16 workgroups, longer chains)
+__global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict__ x, int N, int HW, int C, int Cp,
                                                         const float* __restrict__ w1, const float* __restrict__ b1,
                                                         const float* __restrict__ w2t, const float* __restrict__ b2,
                                                         int sq, float* __restrict__ scale,
                                                         const float* __restrict__ pooled) {
   __shared__ float4 part[kSeThreads];
-  __shared__ __attribute__((aligned(16))) float mean[1024];
-  __shared__ float hid[256];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nq = Cp >> 2;                       // <= 256
-  const int groups = kSeThreads / nq;           // pixel groups sharing a channel quad
-  const float* xb = x + (size_t)n * HW * Cp;
+  __shared__ __attribute__((aligned(16))) float mean[kSeImages * 1024];
+  __shared__ float hid[kSeImages * 256];
+  const int n0 = blockIdx.x * kSeImages, tid = threadIdx.x;
+  const int nimg = min(kSeImages, N - n0);
   if (pooled) {   // means already reduced by the fused expand+depthwise kernel
-    for (int c = tid; c < Cp; c += kSeThreads) mean[c] = pooled[(size_t)n * Cp + c];
+    for (int i = tid; i < kSeImages * Cp; i += kSeThreads) {
+      const int m = i / Cp;
+      mean[i] = m < nimg ? pooled[(size_t)n0 * Cp + i] : 0.f;
+    }
     __syncthreads();
   } else {
-  // (1) pool: thread (q, g) sums pixels g, g + groups, ... -- loads independent
-  {
-    const int q = tid % nq, g = tid / nq;
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-    if (g < groups) {
-      int pix = g;
-      for (; pix + groups < HW; pix += 2 * groups) {
-        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
-        const float4 b = *reinterpret_cast<const float4*>(xb + (size_t)(pix + groups) * Cp + q * 4);
-        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-        s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+    const int nq = Cp >> 2;                       // <= 256
+    const int groups = kSeThreads / nq;           // pixel groups sharing a channel quad
+    for (int m = 0; m < kSeImages; ++m) {
+      if (m >= nimg) {
+        for (int c = tid; c < Cp; c += kSeThreads) mean[m * Cp + c] = 0.f;
+        continue;
       }
-      if (pix < HW) {
-        const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
-        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-      }
-      s0.x += s1.x; s0.y += s1.y; s0.z += s1.z; s0.w += s1.w;
-    }
-    part[tid] = s0;
-  }
-  __syncthreads();
-  if (tid < nq) {
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int g = 0; g < groups; ++g) {
-      const float4 v = part[g * nq + tid];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-    const float hw = (float)HW;
-    *reinterpret_cast<float4*>(mean + tid * 4) = make_float4(t.x / hw, t.y / hw, t.z / hw, t.w / hw);
-  }
-  __syncthreads();
-  }
-  // (2) fc1 + ReLU: wave per output row, lanes split K with 16-byte loads;
-  // up to 3 rows x 4 K-chunks (C <= 1024) issued before the reductions
-  const int nch = (C + 255) / 256;
-  for (int j0 = wave * 3; j0 < sq; j0 += 16 * 3) {
-    float acc[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int j = j0 + r;
-      if (j < sq) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int c = t * 256 + lane * 4;
-          if (t < nch && c < C) {
-            const float4 wv = *reinterpret_cast<const float4*>(w1 + (size_t)j * C + c);
-            const float4 mv = *reinterpret_cast<const float4*>(mean + c);
-            acc[r] = fmaf(wv.x, mv.x, fmaf(wv.y, mv.y, fmaf(wv.z, mv.z, fmaf(wv.w, mv.w, acc[r]))));
+      const float* xb = x + (size_t)(n0 + m) * HW * Cp;
+      // (1) pool: thread (q, g) sums pixels g, g + groups, ... -- loads independent
+      {
+        const int q = tid % nq, g = tid / nq;
+        float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+        if (g < groups) {
+          int pix = g;
+          for (; pix + groups < HW; pix += 2 * groups) {
+            const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
+            const float4 b = *reinterpret_cast<const float4*>(xb + (size_t)(pix + groups) * Cp + q * 4);
+            s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+            s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
           }
+          if (pix < HW) {
+            const float4 a = *reinterpret_cast<const float4*>(xb + (size_t)pix * Cp + q * 4);
+            s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+          }
+          s0.x += s1.x; s0.y += s1.y; s0.z += s1.z; s0.w += s1.w;
         }
+        part[tid] = s0;
       }
-    }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const float v = wave_sum(acc[r]);
-      if (lane == 0 && j0 + r < sq) hid[j0 + r] = fmaxf(v + b1[j0 + r], 0.f);
+      __syncthreads();
+      if (tid < nq) {
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int g = 0; g < groups; ++g) {
+          const float4 v = part[g * nq + tid];
+          t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        const float hw = (float)HW;
+        *reinterpret_cast<float4*>(mean + m * Cp + tid * 4) = make_float4(t.x / hw, t.y / hw, t.z / hw, t.w / hw);
+      }
+      __syncthreads();
     }
   }
-  __syncthreads();
-  // (3) fc2 + hardsigmoid: thread per output over the transposed weights
-  // (coalesced rows), K unrolled 8-deep with two accumulators
-  for (int c = tid; c < Cp; c += kSeThreads) {
-    float v = 0.f;
-    if (c < C) {
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll 8
-      for (int j = 0; j < sq; j += 2) {
-        a0 = fmaf(w2t[(size_t)j * C + c], hid[j], a0);
-        a1 = fmaf(w2t[(size_t)(j + 1) * C + c], hid[j + 1], a1);
-      }
-      v = kpd_hsigmoid(a0 + a1 + b2[c]);
-    }
-    scale[(size_t)n * Cp + c] = v;
-  }
+  se_fc<kSeThreads, kSeImages>(mean, hid, nimg, C, Cp, w1, b1, w2t, b2, sq, scale + (size_t)n0 * Cp);
 }
 
 // FPN lateral 1x1 conv with a small input width (cin_p <= 32) and 128 outputs,
 // plus the nearest-upsampled top-down residual (backbone.py:33-37).  Pure
 // streaming (it writes the largest tensor of the pass): a thread owns 8 output
 // channels of kLatPix pixels, all their inputs are loaded before the first
-// store, and every store is 16 bytes.  Weights transposed in LDS.  16 x
-// kLatPix pixels per workgroup.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
+// store, and every store is 16 bytes.  Weights transposed in LDS once per
+// workgroup; the grid is capped (kLatBlocks) and each workgroup strides over
+// chunks of 16 x kLatPix pixels, so the weight staging, the barrier and the
+// amax publish are amortised over many chunks.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
 // 32 channels per [hi32 | lo32] 128-byte group (the split FPN conv's K row).
 constexpr int kLatPix = 2;   // pixels per thread (4 doubles the registers and halves occupancy: slower)
+constexpr int kLatBlocks = 2048;
 template <int CIN4>          // cin_p / 4
 __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __restrict__ in,
                                                              const float* __restrict__ w,
@@ -372,7 +438,7 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
                                                              const float* __restrict__ res, int H, int W, int rh,
                                                              int rw, int M, float* __restrict__ out,
                                                              float* __restrict__ amax, const float* __restrict__ sc_in,
-                                                             float maxb, float maxs) {
+                                                             float maxb, float maxs, int nt_store) {
   __shared__ __attribute__((aligned(16))) float sw[32 * 128];
   __shared__ float red[4];
   const int tid = threadIdx.x;
@@ -388,68 +454,76 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
   const float4 b0 = *reinterpret_cast<const float4*>(bias + co), b1 = *reinterpret_cast<const float4*>(bias + co + 4);
   const int HW = H * W;
   const float sy = (float)rh / (float)H, sx = (float)rw / (float)W;
-  // load phase: inputs and residuals of this thread's 4 pixels
-  float4 xin[kLatPix][CIN4];
-  float4 r0[kLatPix], r1[kLatPix];
-  int mm[kLatPix];
-#pragma unroll
-  for (int it = 0; it < kLatPix; ++it) {
-    const int m = blockIdx.x * (16 * kLatPix) + it * 16 + sub;
-    mm[it] = m;
-    r0[it] = r1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < CIN4; ++k) xin[it][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m >= M) continue;
-#pragma unroll
-    for (int k = 0; k < CIN4; ++k) xin[it][k] = *reinterpret_cast<const float4*>(in + (size_t)m * cin_p + k * 4);
-    if (res) {
-      const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
-      const int yy = rh == H ? y : min((int)floorf((float)y * sy), rh - 1);
-      const int xx = rw == W ? x : min((int)floorf((float)x * sx), rw - 1);
-      const float* rp = res + ((size_t)(n * rh + yy) * rw + xx) * 128 + co;
-      r0[it] = *reinterpret_cast<const float4*>(rp);
-      r1[it] = *reinterpret_cast<const float4*>(rp + 4);
-    }
-  }
   float m_abs = 0.f;
+  const int chunks = (M + 16 * kLatPix - 1) / (16 * kLatPix);
+  for (int chunk = blockIdx.x; chunk < chunks; chunk += gridDim.x) {
+    // load phase: inputs and residuals of this thread's pixels
+    float4 xin[kLatPix][CIN4];
+    float4 r0[kLatPix], r1[kLatPix];
+    int mm[kLatPix];
 #pragma unroll
-  for (int it = 0; it < kLatPix; ++it) {
-    const int m = mm[it];
-    if (m >= M) continue;
-    float a[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    for (int it = 0; it < kLatPix; ++it) {
+      const int m = chunk * (16 * kLatPix) + it * 16 + sub;
+      mm[it] = m;
+      r0[it] = r1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int k4 = 0; k4 < CIN4; ++k4) {
-      const float xs[4] = {xin[it][k4].x, xin[it][k4].y, xin[it][k4].z, xin[it][k4].w};
+      for (int k = 0; k < CIN4; ++k) xin[it][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m >= M) continue;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 w0 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co);
-        const float4 w1 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co + 4);
-        a[0] = fmaf(xs[q], w0.x, a[0]); a[1] = fmaf(xs[q], w0.y, a[1]);
-        a[2] = fmaf(xs[q], w0.z, a[2]); a[3] = fmaf(xs[q], w0.w, a[3]);
-        a[4] = fmaf(xs[q], w1.x, a[4]); a[5] = fmaf(xs[q], w1.y, a[5]);
-        a[6] = fmaf(xs[q], w1.z, a[6]); a[7] = fmaf(xs[q], w1.w, a[7]);
+      for (int k = 0; k < CIN4; ++k) xin[it][k] = *reinterpret_cast<const float4*>(in + (size_t)m * cin_p + k * 4);
+      if (res) {
+        const int n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+        const int yy = rh == H ? y : min((int)floorf((float)y * sy), rh - 1);
+        const int xx = rw == W ? x : min((int)floorf((float)x * sx), rw - 1);
+        const float* rp = res + ((size_t)(n * rh + yy) * rw + xx) * 128 + co;
+        r0[it] = *reinterpret_cast<const float4*>(rp);
+        r1[it] = *reinterpret_cast<const float4*>(rp + 4);
       }
     }
-    a[0] += r0[it].x; a[1] += r0[it].y; a[2] += r0[it].z; a[3] += r0[it].w;
-    a[4] += r1[it].x; a[5] += r1[it].y; a[6] += r1[it].z; a[7] += r1[it].w;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m_abs = fmaxf(m_abs, fabsf(a[e]));
-    if (sc_in) {
-      typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
-      f16x8v hi, lo;
+    for (int it = 0; it < kLatPix; ++it) {
+      const int m = mm[it];
+      if (m >= M) continue;
+      float a[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xsc = a[e] * sa;
-        hi[e] = (_Float16)xsc;
-        lo[e] = (_Float16)(xsc - (float)hi[e]);
+      for (int k4 = 0; k4 < CIN4; ++k4) {
+        const float xs[4] = {xin[it][k4].x, xin[it][k4].y, xin[it][k4].z, xin[it][k4].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 w0 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co);
+          const float4 w1 = *reinterpret_cast<const float4*>(sw + (k4 * 4 + q) * 128 + co + 4);
+          a[0] = fmaf(xs[q], w0.x, a[0]); a[1] = fmaf(xs[q], w0.y, a[1]);
+          a[2] = fmaf(xs[q], w0.z, a[2]); a[3] = fmaf(xs[q], w0.w, a[3]);
+          a[4] = fmaf(xs[q], w1.x, a[4]); a[5] = fmaf(xs[q], w1.y, a[5]);
+          a[6] = fmaf(xs[q], w1.z, a[6]); a[7] = fmaf(xs[q], w1.w, a[7]);
+        }
       }
-      _Float16* o16 = reinterpret_cast<_Float16*>(out) + (size_t)m * 256 + (co >> 5) * 64 + (co & 31);
-      *reinterpret_cast<f16x8v*>(o16) = hi;
-      *reinterpret_cast<f16x8v*>(o16 + 32) = lo;
-    } else {
-      float* op = out + (size_t)m * 128 + co;
-      *reinterpret_cast<float4*>(op) = make_float4(a[0], a[1], a[2], a[3]);
-      *reinterpret_cast<float4*>(op + 4) = make_float4(a[4], a[5], a[6], a[7]);
+      a[0] += r0[it].x; a[1] += r0[it].y; a[2] += r0[it].z; a[3] += r0[it].w;
+      a[4] += r1[it].x; a[5] += r1[it].y; a[6] += r1[it].z; a[7] += r1[it].w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m_abs = fmaxf(m_abs, fabsf(a[e]));
+      if (sc_in) {
+        typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+        f16x8v hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xsc = a[e] * sa;
+          hi[e] = (_Float16)xsc;
+          lo[e] = (_Float16)(xsc - (float)hi[e]);
+        }
+        _Float16* o16 = reinterpret_cast<_Float16*>(out) + (size_t)m * 256 + (co >> 5) * 64 + (co & 31);
+        if (nt_store) {   // streamed past the caches (the 400 MB output exceeds L2 + MALL)
+          __builtin_nontemporal_store(hi, reinterpret_cast<f16x8v*>(o16));
+          __builtin_nontemporal_store(lo, reinterpret_cast<f16x8v*>(o16 + 32));
+        } else {
+          *reinterpret_cast<f16x8v*>(o16) = hi;
+          *reinterpret_cast<f16x8v*>(o16 + 32) = lo;
+        }
+      } else {
+        float* op = out + (size_t)m * 128 + co;
+        *reinterpret_cast<float4*>(op) = make_float4(a[0], a[1], a[2], a[3]);
+        *reinterpret_cast<float4*>(op + 4) = make_float4(a[4], a[5], a[6], a[7]);
+      }
     }
   }
   if (amax) {
@@ -486,8 +560,14 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const float* __restr
 hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const float* w, const float* b,
                        float* out, int Ho, int Wo, float* amax, hipStream_t st) {
   const int total = N * Ho * Wo;
-  hipLaunchKernelGGL(stem_kernel, dim3((total + 255) / 256), dim3(256), 0, st, img, N, Cin, H, W, w, b, out,
-                     Ho, Wo, amax);
+  if (Cin == 3)
+    hipLaunchKernelGGL(stem_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
+                       Wo, amax);
+  else if (Cin == 1)
+    hipLaunchKernelGGL(stem_kernel<1>, dim3((total + 255) / 256), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
+                       Wo, amax);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -508,7 +588,8 @@ hipError_t launch_dwconv(const float* in, const float* w, const float* b, float*
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st, const float* pooled) {
   if (Cp > 1024 || sq > 256 || C % 4 || sq % 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(se_kernel, dim3(N), dim3(kSeThreads), 0, st, x, HW, C, Cp, w1, b1, w2, b2, sq, scale, pooled);
+  hipLaunchKernelGGL(se_kernel, dim3((N + kSeImages - 1) / kSeImages), dim3(kSeThreads), 0, st, x, N, HW, C, Cp, w1,
+                     b1, w2, b2, sq, scale, pooled);
   return hipGetLastError();
 }
 
@@ -517,8 +598,12 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
                                  float maxb, float maxs, hipStream_t st) {
   if (cin_p != 16 && cin_p != 32) return hipErrorInvalidValue;
   const int M = N * H * W;
-#define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3((M + 16 * kLatPix - 1) / (16 * kLatPix)), dim3(256), 0, st, in, w, bias, res, H, \
-                                  W, rh, rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs)
+  const int chunks = (M + 16 * kLatPix - 1) / (16 * kLatPix);
+  static const int blocks_env = getenv("KPD_LAT_BLOCKS") ? atoi(getenv("KPD_LAT_BLOCKS")) : kLatBlocks;
+  static const int nt_env = getenv("KPD_LAT_NT") ? atoi(getenv("KPD_LAT_NT")) : 0;
+  const int nblk = std::max(1, std::min(chunks, blocks_env));
+#define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3(nblk), dim3(256), 0, st, in, w, bias, res, H, \
+                                  W, rh, rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs, nt_env)
   switch (cin_p / 4) {
     case 4: LAT(4); break;
     case 8: LAT(8); break;
@@ -536,8 +621,9 @@ hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles
 
 size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
-  return 4 * ((a.we ? (size_t)a.cin_p * a.CS : 0) + (size_t)Pin * a.CS + (size_t)K * K * a.CS +
-              (a.pooled ? (size_t)Po * a.CS : 0));
+  const size_t main = (a.we ? (size_t)a.cin_p * a.CS : 0) + (size_t)Pin * a.CS + (size_t)K * K * a.CS +
+                      (a.pooled ? (size_t)Po * a.CS : 0);
+  return 4 * main;
 }
 
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {

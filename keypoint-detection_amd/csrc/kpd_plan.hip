@@ -754,7 +754,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   return KPD_OK;
 }
 
-static int ensure_work(kpd_plan* p, const Dims& d, int k) {
+static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   if (p->have_work[k] && p->dims[k] == d) return KPD_OK;
   Work w;
   const size_t need = carve(p, d, nullptr, w);
@@ -790,7 +790,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   const int HWf = d.Hf * d.Wf, TM = split ? conv16_tile_m() : conv_tile_m();
   d.fused_stats = (HWf % TM) == 0;
   d.tiles = d.fused_stats ? HWf / TM : std::min(64, HWf);
-  if (int rc = ensure_work(p, d, k)) return rc;
+  if (int rc = ensure_work(p, d, k, st)) return rc;
   Work& w = p->work[k];
   g_splitk = w.splitk;
   std::map<std::string, std::pair<const void*, size_t>> dbg;
