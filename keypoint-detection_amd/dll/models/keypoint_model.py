@@ -97,14 +97,29 @@ class MultiPersonKeypointModel(nn.Module):
         self.streams = streams          # sub-batch streams for B >= 32 (kpd_plan_set_streams)
         self._plan: Optional[_native.Plan] = None
         self._plan_key = None
+        self._state_tensors: Optional[List[torch.Tensor]] = None
         if config.num_keypoints != 17 or config.heatmap_head.in_channels != 64 \
                 or config.backbone.out_channels != 128:
             raise ValueError("the native path is built for 17 keypoints, 64 selected channels, 128 FPN channels")
 
     # ------------------------------------------------------------------ plan
     def _weights_key(self, device: torch.device) -> Tuple:
-        vers = tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        # The state tensors are listed once (a module walk costs ~0.7 ms per
+        # forward); storage or in-place changes show in (data_ptr, _version).
+        # Replacing a Parameter object goes through load_state_dict / _apply
+        # (both reset the list) or needs invalidate_plan().
+        if self._state_tensors is None:
+            self._state_tensors = list(self.state_dict(keep_vars=True).values())
+        vers = tuple((t.data_ptr(), t._version) for t in self._state_tensors)
         return (device, self.precision, self.streams, vers)
+
+    def _apply(self, fn, *args, **kwargs):
+        self._state_tensors = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def load_state_dict(self, *args, **kwargs):
+        self._state_tensors = None
+        return super().load_state_dict(*args, **kwargs)
 
     def native_plan(self, device: torch.device) -> _native.Plan:
         """Build (or reuse) the packed-weight plan for ``device``."""
@@ -122,7 +137,7 @@ class MultiPersonKeypointModel(nn.Module):
         return self._plan
 
     def invalidate_plan(self) -> None:
-        self._plan, self._plan_key = None, None
+        self._plan, self._plan_key, self._state_tensors = None, None, None
 
     # ------------------------------------------------------------------ forward
     def forward(self, batch) -> Dict[str, torch.Tensor]:
