@@ -150,7 +150,14 @@ __global__ __launch_bounds__(256) void kh_final_kernel(const float* __restrict__
   __shared__ float sh[256];
   const int r = blockIdx.x;
   const int sl = slot[r];
-  if (sl < 0) return;
+  if (sl < 0) {   // padding slot: zeros
+    const size_t o = (size_t)((r / P) * P + slot_pos(sl)) * 17;
+    for (int i = threadIdx.x; i < 17 * 5; i += blockDim.x) {
+      if (i < 34) kh_kpts[o * 2 + i] = 0.f;
+      else kh_vis[o * 3 + (i - 34)] = 0.f;
+    }
+    return;
+  }
   const size_t o = (size_t)((r / P) * P + sl) * 17;
   ln_linear_sigmoid(lin_r + (size_t)r * r_stride, 256, ln_rg, ln_rb, w_r, b_r, 34, kh_kpts + o * 2, sh);
   ln_linear_sigmoid(lin_v + (size_t)r * v_stride, 128, ln_vg, ln_vb, w_v, b_v, 51, kh_vis + o * 3, sh);

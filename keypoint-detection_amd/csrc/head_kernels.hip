@@ -69,18 +69,25 @@ __global__ __launch_bounds__(128) void topk_kernel(const float* __restrict__ sta
 // ---------------------------------------------------------------- slot map
 // One thread per image: compaction of non-zero boxes (keypoint_model.py:149-153),
 // and the "no valid person" dummy (vis class 0 = 1, :171-179).
-__global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, int32_t* __restrict__ slot,
-                               float* __restrict__ vis_out) {
+__global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, int32_t* __restrict__ slot) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int cnt = 0;
   for (int p = 0; p < P; ++p) {
     const float* bx = boxes + ((size_t)b * P + p) * 4;
-    const bool zero = bx[0] == 0.f && bx[1] == 0.f && bx[2] == 0.f && bx[3] == 0.f;
-    slot[b * P + p] = zero ? -1 : cnt++;
+    if (!(bx[0] == 0.f && bx[1] == 0.f && bx[2] == 0.f && bx[3] == 0.f)) ++cnt;
   }
-  if (cnt == 0 && P > 0)
-    for (int k = 0; k < NK; ++k) vis_out[((size_t)b * P * NK + k) * 3 + 0] = 1.f;
+  int valid = 0, empty = cnt;
+  for (int p = 0; p < P; ++p) {
+    const float* bx = boxes + ((size_t)b * P + p) * 4;
+    const bool zero = bx[0] == 0.f && bx[1] == 0.f && bx[2] == 0.f && bx[3] == 0.f;
+    if (zero) {
+      slot[b * P + p] = slot_empty(empty, cnt == 0 && empty == 0);   // the dummy person sits at position 0
+      ++empty;
+    } else {
+      slot[b * P + p] = valid++;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- ROI align
@@ -279,7 +286,13 @@ __global__ __launch_bounds__(64) void hm_final_kernel(const float* __restrict__ 
   __shared__ float sb[NK];
   const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
   const int sl = slot[r];
-  if (sl < 0) return;  // all-zero box: skipped by the reference
+  if (sl < 0) {   // all-zero box (skipped by the reference): its padding slot gets zeros
+    if (x < HM) {
+      float* dst = heat_out + ((size_t)((r / P) * P + slot_pos(sl)) * NK) * HMP + y * HM + x;
+      for (int k = 0; k < NK; ++k) dst[(size_t)k * HMP] = 0.f;
+    }
+    return;
+  }
   for (int i = x; i < NK * TOPK; i += 64) sw[i] = w[i];
   if (x < NK) sb[x] = b[x];
   __syncthreads();
@@ -312,8 +325,18 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
                                                     float* __restrict__ kpts_out, float* __restrict__ vis_out) {
   const int r = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
   const int sl = slot[r];
-  if (sl < 0) return;
   const int bimg = r / P;
+  if (sl < 0) {   // padding slot: zeros; the dummy person of a box-less image is visibility class 0
+    if (lane == 0) {
+      const size_t o = (size_t)(bimg * P + slot_pos(sl)) * NK + k;
+      kpts_out[o * 2 + 0] = 0.f;
+      kpts_out[o * 2 + 1] = 0.f;
+      vis_out[o * 3 + 0] = slot_dummy(sl) ? 1.f : 0.f;
+      vis_out[o * 3 + 1] = 0.f;
+      vis_out[o * 3 + 2] = 0.f;
+    }
+    return;
+  }
   const size_t o = (size_t)(bimg * P + sl) * NK;
   const float cx = boxes[r * 4 + 0], cy = boxes[r * 4 + 1], bw = boxes[r * 4 + 2], bh = boxes[r * 4 + 3];
   {
@@ -363,8 +386,9 @@ hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float
   hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(FC), 0, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores);
   return hipGetLastError();
 }
-hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, float* vis_out, hipStream_t st) {
-  hipLaunchKernelGGL(slotmap_kernel, dim3((B + 63) / 64), dim3(64), 0, st, boxes, B, P, slot, vis_out);
+hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipStream_t st) {
+  if (P > 0xFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(slotmap_kernel, dim3((B + 63) / 64), dim3(64), 0, st, boxes, B, P, slot);
   return hipGetLastError();
 }
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk, const float* boxes,

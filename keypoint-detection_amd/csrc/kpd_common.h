@@ -41,6 +41,14 @@ __device__ __forceinline__ float wave_max(float v) {
 // whole grid spread over L2 channels instead of queueing on one address.
 // Readers take the max over the slots.  The caller zeroes the slots.
 constexpr int kAmaxSlots = 64, kAmaxStride = 32;
+// Output slot of an ROI: >= 0 = compacted position of a valid box; an
+// all-zero box gets -1 - (pos | dummy << 16), pos = its padding position
+// (after the image's valid boxes), dummy = the image has no valid box (the
+// reference's dummy person, keypoint_model.py:171-199).
+__host__ __device__ __forceinline__ int slot_empty(int pos, bool dummy) { return -1 - (pos | (dummy ? 0x10000 : 0)); }
+__device__ __forceinline__ int slot_pos(int s) { return (-1 - s) & 0xFFFF; }
+__device__ __forceinline__ bool slot_dummy(int s) { return ((-1 - s) >> 16) & 1; }
+
 __device__ __forceinline__ void amax_publish(float* slots, float v) {
   if (v > 0.f)
     atomicMax(reinterpret_cast<unsigned int*>(slots + (blockIdx.x % kAmaxSlots) * kAmaxStride), __float_as_uint(v));

@@ -90,7 +90,7 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
 // ---- channel attention / ROI / heatmap head / decode (head_kernels.hip) ----
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st);
-hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, float* vis_out,
+hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
                             const float* boxes, int R, int P, float* roi, float* roi_stats,

@@ -911,13 +911,11 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
 
   // ---------------- per-ROI heads ----------------
   float* heat_out = heat ? heat : w.heat;
-  const size_t nkp = (size_t)R * 17;
-  HIP_TRY(hipMemsetAsync(kpts, 0, nkp * 2 * sizeof(float), st));
-  HIP_TRY(hipMemsetAsync(vis, 0, nkp * 3 * sizeof(float), st));
-  HIP_TRY(hipMemsetAsync(heat_out, 0, nkp * 3136 * sizeof(float), st));
+  // no output memsets: the padding slots are written (zeros / dummy person) by
+  // hm_final_kernel, decode_kernel and kh_final_kernel through the slot map
   {
     Stage sg(p, "roi_align", st);
-    HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, vis, st));
+    HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
   }
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
@@ -945,8 +943,6 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
     Stage sg(p, "keypoint_head", st);
     const size_t px = (size_t)R * 3136;
-    HIP_TRY(hipMemsetAsync(kh_kpts, 0, nkp * 2 * sizeof(float), st));
-    HIP_TRY(hipMemsetAsync(kh_vis, 0, nkp * 3 * sizeof(float), st));
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
     if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
       return rc;
