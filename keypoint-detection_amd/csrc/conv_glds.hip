@@ -31,9 +31,13 @@
 //   * S-stage ring with a counted s_waitcnt vmcnt and a raw s_barrier: S-1
 //     K-tiles are in flight while the MFMAs of the current one run, and the
 //     single barrier per K-tile never drains the pipeline.
-//   * Epilogue: the accumulator tile is staged through LDS (conv_epilogue.h)
-//     for 16-byte row stores, fused bias / ReLU / unscale / channel sum+max.
+//   * Epilogue (fp32 out) straight from the accumulators: fused bias / ReLU /
+//     unscale, channel sum+max by cross-lane reduction (+ a 2*WAVES_M*BN-float
+//     LDS exchange), and a DPP quad transpose for 16-byte row stores; bf16
+//     outputs stage the tile through LDS (conv_epilogue.h), which measured
+//     faster for them.
 #include <algorithm>
+#include <type_traits>
 
 #include "kpd_common.h"
 #include "kpd_kernels.h"
@@ -77,8 +81,31 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// 4x4 transpose inside each quad of lanes: lane t holds v[e] = C[e][t] of a
+// 4x4 block on entry and C[t][e] on exit (two DPP butterflies, xor 1 / xor 2).
+// Turns a 16x16 MFMA accumulator (a lane = 4 rows of one column) into a lane =
+// 4 consecutive columns of one row, i.e. one 16-byte store per row piece.
+__device__ __forceinline__ float dpp_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_xor2(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ void quad_transpose(f32x4& v, int t) {
+  const bool b0 = t & 1, b1 = t & 2;
+  float r = dpp_xor1(b0 ? v[0] : v[1]);
+  if (b0) v[0] = r; else v[1] = r;
+  r = dpp_xor1(b0 ? v[2] : v[3]);
+  if (b0) v[2] = r; else v[3] = r;
+  r = dpp_xor2(b1 ? v[0] : v[2]);
+  if (b1) v[0] = r; else v[2] = r;
+  r = dpp_xor2(b1 ? v[1] : v[3]);
+  if (b1) v[1] = r; else v[3] = r;
+}
+
 // DBG (kpd_bench_conv16 only): 1 = no LDS-DMA in the K loop, 2 = no MFMA,
-// 4 = every block reads the same 256 A rows (L2-resident working set)
+// 4 = every block reads the same 256 A rows (L2-resident working set),
+// 8 = no epilogue (one value per lane stored), 16 = no K loop
 template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF, int DBG = 0>
 __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
@@ -86,9 +113,15 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   constexpr int A_LD = 4, B_LD = BN / 64;          // LDS-DMA wave-instructions per K-tile per wave
   constexpr int LPT = A_LD + B_LD;
   constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int RING = S * STAGE;
+  // bf16 outputs keep the LDS-staged epilogue (conv_epilogue.h: measured 3%
+  // faster there); fp32 outputs use the register epilogue (1% faster on
+  // FPN0).  DBG 4096 forces the staged one for A/B runs.
+  constexpr bool STAGED = !std::is_same<TO, float>::value || (DBG & 4096) != 0;
   constexpr int EPI_BN = BN > 128 ? 128 : BN;
-  constexpr int EPI = epi_lds_bytes<BM, EPI_BN, NT>();
-  constexpr int LDS = S * STAGE > EPI ? S * STAGE : EPI;
+  constexpr int EPI = STAGED ? epi_lds_bytes<BM, EPI_BN, NT>() : 0;
+  constexpr int LDS_REG = RING + 2 * WAVES_M * BN * 4;   // ring + the register epilogue's statistics exchange
+  constexpr int LDS = LDS_REG > EPI ? LDS_REG : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(S >= 2 && (S - 2) * LPT < 64, "stages");
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -135,7 +168,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
     b_off[i] = (unsigned)((co * KS * KS * cin_e) * 2 + lchunk * 16);
   }
   const int kc_per_tap = cin_e / 64;
-  const int KT = KS * KS * kc_per_tap;
+  const int KT = (DBG & 16) ? 0 : KS * KS * kc_per_tap;
 
   // loader state (wave-uniform): next K-tile to issue as (tap, kc)
   int ld_tap = 0, ld_kc = 0;
@@ -278,24 +311,104 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
       is = is + 1 == S ? 0 : is + 1;
     }
   }
-  __syncthreads();   // every wave's last LDS read done before the epilogue reuses LDS
+  __syncthreads();   // all waves leave the K loop together (measured: the stores of early waves slow the rest)
+  if constexpr ((DBG & 8) != 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    reinterpret_cast<float*>(p.out)[(size_t)blockIdx.x * NT + tid] = s;
+    return;
+  }
 
   // ---------------- epilogue ----------------
   float scale = 1.f;
   if constexpr (SPLIT) scale = ldexpf(1.f, -(split_a_exp(p.sc_in, p.sc_maxb, p.sc_maxs) + p.w_exp));
-  EpiArgs e;
-  e.bias = p.bias; e.out = p.out; e.res = nullptr; e.stats = p.stats; e.amax = nullptr; e.scale = scale;
-  e.M = M; e.H = H; e.W = W; e.cout_p = p.cout_p; e.out_cstride = p.out_cstride; e.rh = H; e.rw = W;
-  e.act = p.act; e.tiles_per_img = p.tiles_per_img;
-  e.post_scale = nullptr; e.post_shift = nullptr; e.act2 = 0; e.act3 = 0;
-  float* tile = reinterpret_cast<float*>(lds);
-  constexpr int HALVES = BN / EPI_BN, WN_PER = EPI_BN / 64;
+  if constexpr (STAGED) {
+    EpiArgs e;
+    e.bias = p.bias; e.out = p.out; e.res = nullptr; e.stats = p.stats; e.amax = nullptr; e.scale = scale;
+    e.M = M; e.H = H; e.W = W; e.cout_p = p.cout_p; e.out_cstride = p.out_cstride; e.rh = H; e.rw = W;
+    e.act = p.act; e.tiles_per_img = p.tiles_per_img;
+    e.post_scale = nullptr; e.post_shift = nullptr; e.act2 = 0; e.act3 = 0;
+    float* tile = reinterpret_cast<float*>(lds);
+    constexpr int HALVES = BN / EPI_BN, WN_PER = EPI_BN / 64;
 #pragma unroll
-  for (int h = 0; h < HALVES; ++h) {
-    if (h) __syncthreads();
-    if (wn / WN_PER == h) acc_to_lds<FM, FN, WM, 64, EPI_BN>(tile, acc, wm, wn % WN_PER, lane);
-    tile_store<TO, BM, EPI_BN, NT>(tile, e, m0, n0 + h * EPI_BN);
+    for (int h = 0; h < HALVES; ++h) {
+      if (h) __syncthreads();
+      if (wn / WN_PER == h) acc_to_lds<FM, FN, WM, 64, EPI_BN>(tile, acc, wm, wn % WN_PER, lane);
+      tile_store<TO, BM, EPI_BN, NT>(tile, e, m0, n0 + h * EPI_BN);
+    }
+    return;
   }
+  // Register epilogue: bias / activation / unscale on the accumulators, the
+  // per-tile channel sum+max (top-k statistics) from cross-lane reductions and
+  // a small LDS exchange between the WAVES_M waves of a column block, then a
+  // DPP quad transpose so each lane stores 16 bytes of one output row.  No
+  // LDS staging of the tile, so the ring can stay as it is.
+  const int t4 = lane & 3, q4 = r16 >> 2;
+  const bool stats = (DBG & 128) == 0 && p.stats != nullptr;   // requires H*W % BM == 0
+  float* sts = reinterpret_cast<float*>(lds + RING);            // [2][WAVES_M][BN]
+  TO* out = reinterpret_cast<TO*>(p.out);
+  // (1) bias + act in place, per-column partials (sum, max) of this wave's
+  // rows: lanes 0-15 after the xor-16/32 reductions
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wn * 64 + j * 16;
+    const float bj = p.bias[col + r16];
+    float sm = 0.f, mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = kpd_act(acc[i][j][e] * scale + bj, p.act);
+        acc[i][j][e] = v;
+        sm += v;
+        mx = fmaxf(mx, v);
+      }
+    if (stats) {
+      sm += __shfl_xor(sm, 16);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      sm += __shfl_xor(sm, 32);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      if (g == 0) {
+        sts[wm * BN + wn * 64 + j * 16 + r16] = sm;
+        sts[(WAVES_M + wm) * BN + wn * 64 + j * 16 + r16] = mx;
+      }
+    }
+  }
+  // (2) combine the WAVES_M row blocks in a fixed order -- before any output
+  // store is issued: a barrier behind the stores waits for the slowest wave's
+  // store queue (measured +4 us per tile)
+  if (stats) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // LDS-only barrier (no vmcnt wait)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tid < BN) {
+      float sm = sts[tid], mx = sts[WAVES_M * BN + tid];
+#pragma unroll
+      for (int w = 1; w < WAVES_M; ++w) {
+        sm += sts[w * BN + tid];
+        mx = fmaxf(mx, sts[(WAVES_M + w) * BN + tid]);
+      }
+      const int n = m0 / HW, t = (m0 - n * HW) / BM;
+      float* st = p.stats + ((size_t)n * p.tiles_per_img + t) * 2 * p.cout_p;
+      st[n0 + tid] = sm;
+      st[p.cout_p + n0 + tid] = mx;
+    }
+  }
+  // (3) transposed 16-byte row stores
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      f32x4 v = acc[i][j];
+      quad_transpose(v, t4);
+      const int row = m0 + wm * WM + i * 16 + g * 4 + t4;
+      if (row < M)
+        store4<TO>(out + (size_t)row * p.out_cstride + n0 + wn * 64 + j * 16 + q4 * 4,
+                   make_float4(v[0], v[1], v[2], v[3]));
+    }
 }
 
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
@@ -367,11 +480,13 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
   const int cin_e = split ? 2 * cin : cin;
   const long in_b = M * cin_e * 2, w_b = (long)cout * 9 * cin_e * 2, out_b = M * cout * 4;
   if (in_b > kMaxDesc) return -1;
-  void *in = nullptr, *wt = nullptr, *out = nullptr, *bias = nullptr, *sc = nullptr;
+  void *in = nullptr, *wt = nullptr, *out = nullptr, *bias = nullptr, *sc = nullptr, *stats = nullptr;
+  const bool with_stats = split && ((long)H * W) % BM == 0;   // as FPN0 runs: top-k statistics fused
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = -2;
   if (hipMalloc(&in, in_b) != hipSuccess || hipMalloc(&wt, w_b) != hipSuccess || hipMalloc(&out, out_b) != hipSuccess ||
-      hipMalloc(&bias, cout * 4) != hipSuccess || hipMalloc(&sc, 2 * kAmaxSlots * kAmaxStride * 4) != hipSuccess)
+      hipMalloc(&bias, cout * 4) != hipSuccess || hipMalloc(&sc, 2 * kAmaxSlots * kAmaxStride * 4) != hipSuccess ||
+      (with_stats && hipMalloc(&stats, (size_t)N * (H * W / BM) * 2 * cout * 4) != hipSuccess))
     goto done;
   (void)hipMemset(in, 0x3C, in_b);
   (void)hipMemset(wt, 0x3A, w_b);
@@ -381,6 +496,7 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
   a.cout_p = cout; a.in_cstride = cin_e; a.out_cstride = cout; a.act = ACT_RELU; a.M = (int)M;
   a.sc_in = (const float*)sc; a.sc_maxb = 1.f; a.sc_maxs = 1.f;
   a.in_bytes = (int)in_b; a.wt_bytes = (int)w_b;
+  if (with_stats) { a.stats = (float*)stats; a.tiles_per_img = H * W / BM; }
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) goto done;
   for (int it = -2; it < iters; ++it) {
     if (it == 0) (void)hipEventRecord(e0, 0);
@@ -390,6 +506,11 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
       case 1: e = bench_launch<1>(a, split, 0); break;
       case 2: e = bench_launch<2>(a, split, 0); break;
       case 4: e = bench_launch<4>(a, split, 0); break;
+      case 8: e = bench_launch<8>(a, split, 0); break;
+      case 16: e = bench_launch<16>(a, split, 0); break;
+      case 24: e = bench_launch<24>(a, split, 0); break;
+      case 128: e = bench_launch<128>(a, split, 0); break;
+      case 4096: e = bench_launch<4096>(a, split, 0); break;
       default: e = hipErrorInvalidValue;
     }
     if (e != hipSuccess) goto done;
@@ -403,5 +524,6 @@ done:
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   (void)hipFree(in); (void)hipFree(wt); (void)hipFree(out); (void)hipFree(bias); (void)hipFree(sc);
+  (void)hipFree(stats);
   return rc;
 }

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Ablation timings of the LDS-DMA conv (kpd_bench_conv16): full kernel, no
-K-loop loads, no MFMAs, L2-resident A.  Prints one JSON line per case."""
+K-loop loads, no MFMAs, L2-resident A, no epilogue, no K loop.  Prints one
+JSON line per case (argv[1]: comma-separated dbg values)."""
 import ctypes
 import json
 import sys
@@ -14,10 +15,13 @@ CASES = [  # (label, split, N, H, W, cin, cout, flop)
     ("fpn0_split", 1, 64, 128, 96, 128, 128, 2 * 64 * 128 * 96 * 128 * 128 * 9 * 3),
     ("hm2_bf16", 0, 64, 56, 56, 256, 256, 2 * 64 * 56 * 56 * 256 * 256 * 9),
 ]
+# warm-up (clocks / caches): the first timed case of a process otherwise reads ~5% slow
 for label, split, N, H, W, cin, cout, flop in CASES:
-    for dbg in (0, 1, 2, 4):
+    lib.kpd_bench_conv16(split, N, H, W, cin, cout, 0, 30, ctypes.byref(ctypes.c_float(0)))
+for label, split, N, H, W, cin, cout, flop in CASES:
+    for dbg in [int(v) for v in (sys.argv[1].split(',') if len(sys.argv) > 1 else '0,1,2,4,8,16,24'.split(','))]:
         ms = ctypes.c_float(0)
-        rc = lib.kpd_bench_conv16(split, N, H, W, cin, cout, dbg, 20, ctypes.byref(ms))
+        rc = lib.kpd_bench_conv16(split, N, H, W, cin, cout, dbg, 40, ctypes.byref(ms))
         print(json.dumps({"case": label, "dbg": dbg, "rc": rc, "ms": round(ms.value, 4),
                           "mfma_tflops": round(flop / (ms.value * 1e-3) / 1e12, 1) if rc == 0 and ms.value else None}),
               flush=True)
