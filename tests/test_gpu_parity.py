@@ -291,3 +291,28 @@ def test_sub_batch_streams_match(model_sd, precision):
         # bf16 heatmap head can turn into a bf16 ulp here and there
         torch.testing.assert_close(a["keypoints"], b["keypoints"], atol=1e-3, rtol=0)
         torch.testing.assert_close(a["heatmap"], b["heatmap"], atol=3e-2, rtol=0)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_c5_shape_dual_head_vs_oracle(precision):
+    """BASELINE config C5's shape at a CPU-checkable batch: 384x288 input
+    (FPN0 map 192x144 -> 108 M-tiles per image), 5 boxes per image with zero
+    padding slots, heatmap head + KEYPOINT_HEAD."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m, sd = _dual_model(precision)
+    img = synthetic_images(2, 3, 384, 288, seed=51)
+    boxes = synthetic_boxes(2, 5, seed=52)
+    boxes[0, 3:] = 0.0                     # two padding slots in image 0
+    with torch.no_grad():
+        out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    ref = O.forward(sd, {"image": img, "bboxes": boxes}, dual_head=True)
+    tol_k, tol_h = (1e-5, 5e-5) if precision == "fp32" else (1e-3, 3e-2)
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=tol_k)
+    np.testing.assert_allclose(out["heatmap"].cpu().numpy(), ref["heatmap"].numpy(), atol=tol_h)
+    if precision == "fp32":
+        assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
+    else:   # bf16 heads: visibility class flips bounded as in the module docstring
+        flips = (out["visibilities"].cpu() != ref["visibilities"]).any(-1).float().mean().item()
+        assert flips <= 0.02
+    np.testing.assert_allclose(out["kh_keypoints"].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol_k)
+    np.testing.assert_allclose(out["kh_visibilities"].cpu().numpy(), ref["kh_visibilities"].numpy(), atol=tol_k)
