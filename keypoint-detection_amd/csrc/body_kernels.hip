@@ -349,6 +349,191 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   }
 }
 
+// Fused MobileNetV3 inverted residual without SE (features.2 / features.3 of
+// mobilenet_v3_small, backbone.py:250-254): expand 1x1 + act, depthwise KxK
+// stride S + act, project 1x1 (+ residual), on a tile of TH output rows x the
+// full width of one image.  The expanded channels are processed in slices of
+// FIR_CS: a slice is expanded (input rows of the tile incl. the depthwise halo,
+// zero outside the image), filtered, and folded into the project accumulators
+// that each thread keeps for 2 pixels x 8 output channels -- the expanded and
+// depthwise tensors never touch HBM (the unfused path writes and re-reads
+// them: 2 launches and ~75 MB per step at 256x192).  Sums run in a fixed order
+// (input channel, tap, expanded channel), so results do not depend on the batch.
+constexpr int FIR_CS = 16;
+template <int K, int S>
+__global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int PD = (K - 1) / 2, CS = FIR_CS, CQ = CS / 4;
+  const int n = blockIdx.y, oy0 = blockIdx.x * a.TH, tid = threadIdx.x;
+  const int TH = min(a.TH, a.Ho - oy0), Wi = a.Wi, Wo = a.Wo, cin_p = a.cin_p, cout_p = a.cout_p;
+  const int iy0 = oy0 * S - PD, THin = (a.TH - 1) * S + K;
+  const int npx_in = THin * Wi, npx = TH * Wo;
+  // LDS: [xs: npx_in x cin_p] [es: npx_in x CS] [ds: TH*Wo x CS] [weT: cin_p x CS] [wds: K*K x CS] [wpT: CS x cout_p]
+  float* xs = sm;
+  float* es = xs + npx_in * cin_p;
+  float* ds = es + npx_in * CS;
+  float* weT = ds + a.TH * Wo * CS;
+  float* wds = weT + cin_p * CS;
+  float* wpT = wds + K * K * CS;
+  // the input rows of the tile (zero outside the image)
+  const float* xg = a.x + (size_t)n * a.Hi * Wi * cin_p;
+  const int cq_in = cin_p / 4;
+  for (int i = tid; i < npx_in * cq_in; i += 256) {
+    const int px = i / cq_in, q = i - px * cq_in, iy = iy0 + px / Wi;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (iy >= 0 && iy < a.Hi) v = *reinterpret_cast<const float4*>(xg + ((size_t)iy * Wi + px % Wi) * cin_p + q * 4);
+    reinterpret_cast<float4*>(xs)[i] = v;
+  }
+  // project accumulators: unit = (pixel pair, 8 output channels)
+  const int nco8 = cout_p / 8, npair = (npx + 1) / 2, units = npair * nco8;
+  const bool has_unit = tid < units;
+  const int u_pair = tid / nco8, u_co = (tid - u_pair * nco8) * 8;
+  const int px0 = min(u_pair * 2, npx - 1), px1 = min(u_pair * 2 + 1, npx - 1);
+  float acc[2][8];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+
+  for (int c0 = 0; c0 < a.Ep; c0 += CS) {
+    __syncthreads();   // previous slice's es / ds / weights fully consumed (and xs staged)
+    for (int i = tid; i < cin_p * CS; i += 256) {
+      const int c = i / cin_p, k = i - c * cin_p;
+      weT[k * CS + c] = a.we[(size_t)(c0 + c) * cin_p + k];
+    }
+    for (int i = tid; i < K * K * CQ; i += 256) {
+      const int t = i / CQ, q = i - t * CQ;
+      reinterpret_cast<float4*>(wds)[i] = *reinterpret_cast<const float4*>(a.wd + (size_t)t * a.Ep + c0 + q * 4);
+    }
+    for (int i = tid; i < CS * cout_p; i += 256) {
+      const int co = i / CS, c = i - co * CS;
+      wpT[c * cout_p + co] = a.wp[(size_t)co * a.Ep + c0 + c];
+    }
+    __syncthreads();
+    // expand: 4 pixels x 4 channels per thread, weights from LDS
+    const int pg_n = (npx_in + 3) / 4;
+    for (int i = tid; i < pg_n * CQ; i += 256) {
+      const int pg = i / CQ, q = i - pg * CQ;
+      const float4 b = *reinterpret_cast<const float4*>(a.be + c0 + q * 4);
+      float acc_e[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { acc_e[r][0] = b.x; acc_e[r][1] = b.y; acc_e[r][2] = b.z; acc_e[r][3] = b.w; }
+      int pxr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pxr[r] = min(pg * 4 + r, npx_in - 1);
+      for (int k = 0; k < cin_p; k += 4) {
+        float4 xv[4], wv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4*>(xs + pxr[r] * cin_p + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = *reinterpret_cast<const float4*>(weT + (k + j) * CS + q * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xk[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc_e[r][0] = fmaf(xk[j], wv[j].x, acc_e[r][0]); acc_e[r][1] = fmaf(xk[j], wv[j].y, acc_e[r][1]);
+            acc_e[r][2] = fmaf(xk[j], wv[j].z, acc_e[r][2]); acc_e[r][3] = fmaf(xk[j], wv[j].w, acc_e[r][3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = pg * 4 + r;
+        if (px >= npx_in) break;
+        const int iy = iy0 + px / Wi;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);   // the depthwise zero padding of the expanded tensor
+        if (iy >= 0 && iy < a.Hi)
+          v = make_float4(kpd_act(acc_e[r][0], a.act_e), kpd_act(acc_e[r][1], a.act_e),
+                          kpd_act(acc_e[r][2], a.act_e), kpd_act(acc_e[r][3], a.act_e));
+        reinterpret_cast<float4*>(es)[px * CQ + q] = v;
+      }
+    }
+    __syncthreads();
+    // depthwise: 4 consecutive output columns x 4 channels per thread
+    constexpr int XT = 4, NC = (XT - 1) * S + K;
+    const int wx = (Wo + XT - 1) / XT;
+    for (int i = tid; i < TH * wx * CQ; i += 256) {
+      const int q = i % CQ, r = i / CQ, xt = r % wx, oy = r / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
+      float4 d[XT];
+#pragma unroll
+      for (int o = 0; o < XT; ++o) d[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        const int ly = oy * S + ky;   // row in the tile (iy = iy0 + ly)
+        float4 col[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int ix = ix0 + c;
+          col[c] = (ix >= 0 && ix < Wi) ? reinterpret_cast<const float4*>(es)[(ly * Wi + ix) * CQ + q]
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const float4 w = reinterpret_cast<const float4*>(wds)[(ky * K + kx) * CQ + q];
+#pragma unroll
+          for (int o = 0; o < XT; ++o) {
+            const float4 v = col[o * S + kx];
+            d[o].x = fmaf(v.x, w.x, d[o].x); d[o].y = fmaf(v.y, w.y, d[o].y);
+            d[o].z = fmaf(v.z, w.z, d[o].z); d[o].w = fmaf(v.w, w.w, d[o].w);
+          }
+        }
+      }
+      const float4 b = *reinterpret_cast<const float4*>(a.bd + c0 + q * 4);
+#pragma unroll
+      for (int o = 0; o < XT; ++o) {
+        if (ox0 + o >= Wo) break;
+        float4 v;
+        v.x = kpd_act(d[o].x + b.x, a.act_d); v.y = kpd_act(d[o].y + b.y, a.act_d);
+        v.z = kpd_act(d[o].z + b.z, a.act_d); v.w = kpd_act(d[o].w + b.w, a.act_d);
+        reinterpret_cast<float4*>(ds)[(oy * Wo + ox0 + o) * CQ + q] = v;
+      }
+    }
+    __syncthreads();
+    // project: fold this slice into the accumulators
+    if (has_unit) {
+#pragma unroll
+      for (int c4 = 0; c4 < CQ; ++c4) {
+        const float4 d0 = reinterpret_cast<const float4*>(ds)[px0 * CQ + c4];
+        const float4 d1 = reinterpret_cast<const float4*>(ds)[px1 * CQ + c4];
+        const float dv0[4] = {d0.x, d0.y, d0.z, d0.w}, dv1[4] = {d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          const float4 w0 = *reinterpret_cast<const float4*>(wpT + (c4 * 4 + cc) * cout_p + u_co);
+          const float4 w1 = *reinterpret_cast<const float4*>(wpT + (c4 * 4 + cc) * cout_p + u_co + 4);
+          const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            acc[0][j] = fmaf(dv0[cc], wv[j], acc[0][j]);
+            acc[1][j] = fmaf(dv1[cc], wv[j], acc[1][j]);
+          }
+        }
+      }
+    }
+  }
+  if (!has_unit) return;
+  const float4 b0 = *reinterpret_cast<const float4*>(a.bp + u_co), b1 = *reinterpret_cast<const float4*>(a.bp + u_co + 4);
+  const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int px = u_pair * 2 + r;
+    if (px >= npx) break;
+    const int oy = oy0 + px / Wo, ox = px % Wo;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = acc[r][j] + bv[j];
+    if (a.res) {   // stride 1: the residual pixel is the output pixel
+      const float* xr = xg + ((size_t)oy * Wi + ox) * cin_p + u_co;
+      const float4 r0 = *reinterpret_cast<const float4*>(xr), r1 = *reinterpret_cast<const float4*>(xr + 4);
+      v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+      v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+    }
+    float* op = a.out + (((size_t)n * a.Ho + oy) * Wo + ox) * cout_p + u_co;
+    *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(op + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 // Squeeze-excitation, one 1024-thread workgroup (16 waves) per kSeImages
 // images (the fc weights are the bulk of the traffic, so each weight load
 // serves several images).  The three steps are dependent, so each is laid
@@ -616,6 +801,39 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st) {
   hipLaunchKernelGGL(channel_stats_kernel, dim3(tiles, N), dim3(128), 0, st, x, HW, Cp, tiles, stats);
+  return hipGetLastError();
+}
+
+size_t fir_lds_bytes(const FirArgs& a, int K, int S) {
+  const size_t THin = (size_t)(a.TH - 1) * S + K;
+  return 4 * (THin * a.Wi * a.cin_p + THin * a.Wi * FIR_CS + (size_t)a.TH * a.Wo * FIR_CS + (size_t)a.cin_p * FIR_CS +
+              (size_t)K * K * FIR_CS + (size_t)FIR_CS * a.cout_p);
+}
+
+int fir_pick_rows(FirArgs& a, int K, int S) {
+  if (a.cin_p % 4 || a.Ep % FIR_CS || a.cout_p % 8 || (a.res && (S != 1 || a.cin_p != a.cout_p))) return 0;
+  static const int th_env = getenv("KPD_FIR_TH") ? atoi(getenv("KPD_FIR_TH")) : 0;   // A/B sweeps
+  for (int th = std::min(a.Ho, th_env > 0 ? th_env : 16); th >= 1; --th) {
+    a.TH = th;
+    const int units = (th * a.Wo + 1) / 2 * (a.cout_p / 8);
+    if (units <= 256 && fir_lds_bytes(a, K, S) <= 64 * 1024) return th;
+  }
+  a.TH = 0;
+  return 0;
+}
+
+hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st) {
+  if (a.TH <= 0 || (a.TH * a.Wo + 1) / 2 * (a.cout_p / 8) > 256) return hipErrorInvalidValue;
+  const size_t lds = fir_lds_bytes(a, K, S);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  const dim3 grid((a.Ho + a.TH - 1) / a.TH, N);
+#define FIR(KK, SS) hipLaunchKernelGGL((fir_kernel<KK, SS>), grid, dim3(256), lds, st, a)
+  if (K == 3 && S == 1) FIR(3, 1);
+  else if (K == 3 && S == 2) FIR(3, 2);
+  else if (K == 5 && S == 1) FIR(5, 1);
+  else if (K == 5 && S == 2) FIR(5, 2);
+  else return hipErrorInvalidValue;
+#undef FIR
   return hipGetLastError();
 }
 

@@ -63,6 +63,23 @@ hipError_t launch_dwconv(const float* in, const float* w, const float* b, float*
 hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* w1, const float* b1,
                      const float* w2, const float* b2, int sq, float* scale, hipStream_t st,
                      const float* pooled = nullptr);
+// fused inverted residual WITHOUT squeeze-excitation on row tiles
+// (body_kernels.hip, fir_kernel): expand 1x1 + act -> depthwise KxK stride S
+// + act -> project 1x1 (+ residual), the expanded tensor never leaves LDS
+struct FirArgs {
+  const float* x;        // NHWC [N][Hi][Wi][cin_p]
+  int Hi, Wi, cin_p;
+  const float *we, *be;  // expand [Ep][cin_p], [Ep] (BN folded)
+  const float *wd, *bd;  // depthwise [K*K][Ep], [Ep]
+  const float *wp, *bp;  // project [cout_p][Ep], [cout_p]
+  int act_e, act_d, Ep, cout_p;
+  float* out;            // NHWC [N][Ho][Wo][cout_p]
+  int Ho, Wo, res;       // res: add x (stride 1, cin_p == cout_p)
+  int TH;                // output rows per workgroup (host-chosen)
+};
+size_t fir_lds_bytes(const FirArgs& a, int K, int S);
+int fir_pick_rows(FirArgs& a, int K, int S);   // sets a.TH; 0 when the layer does not fit
+hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st);
 // fused expand 1x1 + depthwise + channel means (body_kernels.hip, exdw_kernel)
 struct ExDwArgs {
   const float* x;        // NHWC [N][Hi][Wi][cin_p]

@@ -814,6 +814,30 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     xa.out = w.d[i]; xa.Ho = ho; xa.Wo = wo; xa.pooled = bn.cfg.se ? w.pool : nullptr;
     bool fused = false;
     static const bool no_fuse = getenv("KPD_NO_FUSE") != nullptr;   // A/B switch for measurements
+    // no SE: the whole block (expand, depthwise, project, residual) in one kernel on row tiles
+    // fused by default only at stride 2 (features.2: -31 us per step); the stride-1
+    // block (features.3) measured 6 us slower fused than as three kernels.
+    // KPD_FIR_MASK (bit i = block i) overrides for A/B runs.
+    static const int fir_mask = getenv("KPD_FIR_MASK") ? atoi(getenv("KPD_FIR_MASK")) : -1;
+    const bool fir_on = fir_mask < 0 ? bn.cfg.s == 2 : ((fir_mask >> i) & 1) != 0;
+    if (!no_fuse && fir_on && !bn.cfg.se && bn.has_exp && bn.expand.cout_p == bn.dw.Cp &&
+        bn.project.cin_p == bn.dw.Cp) {
+      FirArgs fa{};
+      fa.x = x; fa.Hi = hi; fa.Wi = wi; fa.cin_p = inp;
+      fa.we = static_cast<const float*>(bn.expand.w); fa.be = bn.expand.b;
+      fa.wd = bn.dw.w; fa.bd = bn.dw.b;
+      fa.wp = static_cast<const float*>(bn.project.w); fa.bp = bn.project.b;
+      fa.act_e = bn.cfg.act; fa.act_d = bn.dw.act; fa.Ep = bn.dw.Cp; fa.cout_p = bn.project.cout_p;
+      fa.out = w.o[i]; fa.Ho = ho; fa.Wo = wo;
+      fa.res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
+      if (fir_pick_rows(fa, bn.dw.k, bn.dw.s)) {
+        HIP_TRY(launch_fir(fa, B, bn.dw.k, bn.dw.s, st));
+        x = w.o[i];
+        if (i + 1 == 3) taps[1] = x;
+        if (i + 1 == 8) taps[2] = x;
+        continue;
+      }
+    }
     if (!no_fuse && hi * wi <= kFuseMaxPix && (!bn.has_exp || bn.expand.cout_p == bn.dw.Cp)) {
       for (int cs : {16, 32, 48}) {   // narrow slices: more workgroups for these small layers
         xa.CS = cs;
