@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Ablation timings of the LDS-DMA conv (kpd_bench_conv16): full kernel, no
-K-loop loads, no MFMAs, L2-resident A, no epilogue, no K loop.  Prints one
+"""Ablation timings of the LDS-DMA conv (kpd_bench_conv16): dbg 0 = the
+production dispatch (launch_conv16), 65536 = the BN=128 / 3-stage kernel,
+others = ablations of that kernel (no K-loop loads, no MFMAs, L2-resident A,
+no epilogue, no K loop).  Prints one
 JSON line per case (argv[1]: comma-separated dbg values)."""
 import ctypes
 import json
@@ -13,6 +15,7 @@ from dll import _native  # noqa: E402
 lib = _native.load()
 CASES = [  # (label, split, N, H, W, cin, cout, flop)
     ("fpn0_split", 1, 64, 128, 96, 128, 128, 2 * 64 * 128 * 96 * 128 * 128 * 9 * 3),
+    ("hm1_bf16", 0, 64, 56, 56, 64, 256, 2 * 64 * 56 * 56 * 64 * 256 * 9),
     ("hm2_bf16", 0, 64, 56, 56, 256, 256, 2 * 64 * 56 * 56 * 256 * 256 * 9),
 ]
 # warm-up (clocks / caches): the first timed case of a process otherwise reads ~5% slow
