@@ -411,6 +411,282 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
     }
 }
 
+// ---------------------------------------------------------------- FPN level 0 by linearity
+// out = ReLU(conv3x3(lat0) + b) with lat0 = L0(tap0) + up4(lat1) (backbone.py:
+// 29-39; the 1x1 laterals have no bias).  Linearity splits the conv into
+//   (1) conv3x3 with the composite weights W3.L0 on the 16-channel tap0
+//       (K = 9 taps x 16 = 144 instead of 9 x 128), and
+//   (2) for output pixel (4Y + a, 4X + b) a sum over the lat1 pixels its nine
+//       taps read after the 4x nearest upsample: (Y + oy, X + ox) with the taps
+//       that land there summed into one weight matrix -- 1, 2 or 4 groups of
+//       128 input channels depending on the position class (a, b).
+// Both parts accumulate into the same MFMA tile; the tile's 256 pixels are of
+// ONE class (consecutive lat1-grid pixels of one image), so each K-tile has
+// one B operand.  2.6x fewer MACs than the 3x3 conv over lat0, and lat0 (403
+// MB per step at C2) is never written.  Same fp32-accurate f16 hi/lo products
+// as conv16_kernel<split>; zero padding comes from the buffer range checks
+// (with an exact 4x upsample the taps outside the image are exactly the lat1
+// rows / columns outside the grid).  Register epilogue with the channel
+// statistics; rows past the image's class grid are masked out of them.
+__global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
+  constexpr int BN = 128, S = 3, WAVES_N = 2, WAVES_M = 4;
+  constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
+  constexpr int A_LD = 4, B_LD = BN / 64, LPT = A_LD + B_LD;
+  constexpr int STAGE = (BM + BN) * ROWB, RING = S * STAGE;
+  constexpr int LDS = RING + 2 * WAVES_M * BN * 4;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  constexpr int KT0 = 5;                          // tap0 K-tiles: taps (2k, 2k+1)
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int Hf = p.Hf, Wf = p.Wf, rh = p.rh, rw = p.rw, RG = rh * rw;
+  const int per_cls = p.N * p.tpc;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int cls = L / per_cls, rem = L - cls * per_cls, n = rem / p.tpc, jt = rem - n * p.tpc;
+  const int ca = cls >> 2, cb = cls & 3;
+  const int q0 = jt * BM;                         // first lat1-grid pixel of the tile
+  const int NG = p.cls_ng[cls];
+  const int KT = KT0 + 4 * NG;
+
+  const i32x4 rf = make_rsrc(p.f_split, p.f_bytes), rl = make_rsrc(p.l_split, p.l_bytes);
+  const i32x4 rw0 = make_rsrc(p.w0, p.w0_bytes), rwe = make_rsrc(p.weff, p.weff_bytes);
+  const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
+  const unsigned a_dst = __builtin_amdgcn_readfirstlane(lds0 + wave * 32 * ROWB);
+  const unsigned b_dst = __builtin_amdgcn_readfirstlane(lds0 + (BM + wave * (BN / 8)) * ROWB);
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+
+  // per staged row: tap0 pixel offset (64-byte rows) + 9-tap mask, lat1 pixel
+  // offset (512-byte rows) + group mask
+  unsigned f_off[A_LD], f_mask[A_LD], l_off[A_LD], l_mask[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int q = q0 + wave * 32 + i * 8 + lrow;
+    f_off[i] = l_off[i] = 0;
+    f_mask[i] = l_mask[i] = 0;
+    if (q < RG) {
+      const int Y = q / rw, X = q - Y * rw, y = 4 * Y + ca, x = 4 * X + cb;
+      f_off[i] = (unsigned)((((size_t)n * Hf + y) * Wf + x) * 64);
+      l_off[i] = (unsigned)((((size_t)n * rh + Y) * rw + X) * 512);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy >= 0 && yy < Hf && xx >= 0 && xx < Wf) f_mask[i] |= 1u << t;
+      }
+      for (int g = 0; g < NG; ++g) {
+        const int gg = p.cls_g[cls][g], oy = gg / 3 - 1, ox = gg % 3 - 1;
+        if (Y + oy >= 0 && Y + oy < rh && X + ox >= 0 && X + ox < rw) l_mask[i] |= 1u << g;
+      }
+    }
+  }
+  // this lane's 16-byte piece of a tap0 K-row: chunks 0-1 hi(t1), 2-3 hi(t2),
+  // 4-5 lo(t1), 6-7 lo(t2); a tap0 pixel row is [hi16 | lo16] (64 bytes)
+  const int f_tsel = (lchunk >> 1) & 1;                       // 0: t1, 1: t2
+  const unsigned f_byte = (unsigned)((lchunk >> 2) * 32 + (lchunk & 1) * 16);
+  const int co_b = wave * (BN / 8) + lrow;                     // B rows of this lane (+ 8 i)
+  int ld = 0;                                                  // next K-tile to issue
+  auto issue = [&](int stage) {
+    const unsigned so = stage * STAGE;
+    if (ld < KT0) {
+      const int t = 2 * ld + f_tsel;
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const int delta = (dy * Wf + dx) * 64 + (int)f_byte;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const unsigned voff = (t < 9 && ((f_mask[i] >> t) & 1u)) ? f_off[i] + delta : OOB;
+        glds16(rf, a_dst + so + i * 8 * ROWB, voff, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i)
+        glds16(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + ld) * ROWB + lchunk * 16), 0);
+    } else {
+      const int k = ld - KT0, g = k >> 2, kc = k & 3;
+      const int gg = p.cls_g[cls][g], oy = gg / 3 - 1, ox = gg % 3 - 1;
+      const int delta = (oy * rw + ox) * 512 + kc * 128 + lchunk * 16;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const unsigned voff = ((l_mask[i] >> g) & 1u) ? l_off[i] + delta : OOB;
+        glds16(rl, a_dst + so + i * 8 * ROWB, voff, 0);
+      }
+      const int wbase = p.cls_woff[cls] * 2;   // bytes
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i)
+        glds16(rwe, b_dst + so + i * 8 * ROWB,
+               (unsigned)(wbase + (((co_b + i * 8) * NG + g) * 4 + kc) * ROWB + lchunk * 16), 0);
+    }
+    ++ld;
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+  const int a_row = (wm * WM + r16) * ROWB, b_row = (BM + wn * 64 + r16) * ROWB;
+  const int ch0 = ((g ^ (r16 & 7)) << 4), ch1 = (((4 + g) ^ (r16 & 7)) << 4);
+  struct Frag {
+    uint4 a[2][FM], b[2][FN];
+  };
+  auto load_frags = [&](int stage, Frag& f) {
+    const char* sb = lds + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      f.a[0][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch0);
+      f.a[1][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch1);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      f.b[0][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch0);
+      f.b[1][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch1);
+    }
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
+                                                           __builtin_bit_cast(f16x8, f.b[1][j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[1][i]),
+                                                           __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
+                                                           __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
+  };
+  auto tile_ready = [&](int k) {
+    if (k + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < KT) issue(s);
+  {
+    Frag f0, f1;
+    tile_ready(0);
+    load_frags(0, f0);
+    int is = S - 1, rs = 1;
+    auto step = [&](int kt, Frag& cur, Frag& nxt) {
+      if (kt + S - 1 < KT) issue(is);
+      is = is + 1 == S ? 0 : is + 1;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (kt + 1 < KT) {
+        tile_ready(kt + 1);
+        load_frags(rs, nxt);
+        rs = rs + 1 == S ? 0 : rs + 1;
+      }
+      __builtin_amdgcn_s_setprio(1);
+      mma(cur);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    int kt = 0;
+    for (; kt + 1 < KT; kt += 2) {
+      step(kt, f0, f1);
+      step(kt + 1, f1, f0);
+    }
+    if (kt < KT) step(kt, f0, f1);
+  }
+  __syncthreads();
+
+  // ---------------- register epilogue ----------------
+  int a_f, a_l, P;
+  fpn0x_exps(p.sc, p.w_exp0, p.w_expE, &a_f, &a_l, &P);
+  const float scale = ldexpf(1.f, -P);
+  const int t4 = lane & 3, q4 = r16 >> 2;
+  float* sts = reinterpret_cast<float*>(lds + RING);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wn * 64 + j * 16;
+    const float bj = p.bias[col + r16];
+    float sm = 0.f, mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
+        acc[i][j][e] = v;
+        const bool row_ok = q0 + wm * WM + i * 16 + g * 4 + e < RG;
+        sm += row_ok ? v : 0.f;
+        mx = row_ok ? fmaxf(mx, v) : mx;
+      }
+    sm += __shfl_xor(sm, 16);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    sm += __shfl_xor(sm, 32);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    if (g == 0) {
+      sts[wm * BN + col + r16] = sm;
+      sts[(WAVES_M + wm) * BN + col + r16] = mx;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (tid < BN) {
+    float sm = sts[tid], mx = sts[WAVES_M * BN + tid];
+#pragma unroll
+    for (int w = 1; w < WAVES_M; ++w) {
+      sm += sts[w * BN + tid];
+      mx = fmaxf(mx, sts[(WAVES_M + w) * BN + tid]);
+    }
+    float* st = p.stats + ((size_t)n * 16 * p.tpc + cls * p.tpc + jt) * 2 * BN;
+    st[tid] = sm;
+    st[BN + tid] = mx;
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      f32x4 v = acc[i][j];
+      quad_transpose(v, t4);
+      const int q = q0 + wm * WM + i * 16 + g * 4 + t4;
+      if (q < RG) {
+        const int Y = q / rw, X = q - Y * rw;
+        float* dst = p.out + (((size_t)n * Hf + 4 * Y + ca) * Wf + 4 * X + cb) * BN + wn * 64 + j * 16 + q4 * 4;
+        *reinterpret_cast<f32x4*>(dst) = v;
+      }
+    }
+}
+
+// fp32 rows -> f16 hi|lo rows (groups of G = 32 channels, 16 when cin == 16),
+// scaled by the power of two of operand `which` (0: tap0, 1: lateral 1)
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ in, long npix, int cin,
+                                                         const float* __restrict__ sc, int which, int w_exp0,
+                                                         int w_expE, _Float16* __restrict__ out) {
+  int a_f, a_l, P;
+  fpn0x_exps(sc, w_exp0, w_expE, &a_f, &a_l, &P);
+  const float s = ldexpf(1.f, which ? a_l : a_f);
+  const int G = cin == 16 ? 16 : 32, c8n = cin / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * c8n) return;
+  const long px = i / c8n;
+  const int c = (int)(i - px * c8n) * 8;
+  const float4 u = *reinterpret_cast<const float4*>(in + px * cin + c);
+  const float4 v = *reinterpret_cast<const float4*>(in + px * cin + c + 4);
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+  f16x8v hi, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float xs = x[e] * s;
+    hi[e] = (_Float16)xs;
+    lo[e] = (_Float16)(xs - (float)hi[e]);
+  }
+  _Float16* o = out + px * 2 * cin + (c / G) * 2 * G + c % G;
+  *reinterpret_cast<f16x8v*>(o) = hi;
+  *reinterpret_cast<f16x8v*>(o + G) = lo;
+}
+
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
 
 template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF = (BN <= 128)>
@@ -458,6 +734,23 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
   if (a.cout_p % 64 == 0)
     return out_bf16 ? launch<false, __bf16, 3, 64, 3>(a, st) : launch<false, float, 3, 64, 3>(a, st);
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
+  if (a.N <= 0) return hipSuccess;
+  if (a.Hf != 4 * a.rh || a.Wf != 4 * a.rw || a.tpc != (a.rh * a.rw + BM - 1) / BM) return hipErrorInvalidValue;
+  const long tiles = 16L * a.N * a.tpc;
+  hipLaunchKernelGGL(fpn0x_kernel, dim3((unsigned)tiles), dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_rows(const float* in, long npix, int cin, const float* sc, int which, int w_exp0, int w_expE,
+                             void* out, hipStream_t st) {
+  if (cin != 16 && cin % 32 != 0) return hipErrorInvalidValue;
+  const long n = npix * (cin / 8);
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, npix, cin, sc,
+                     which, w_exp0, w_expE, static_cast<_Float16*>(out));
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- diagnostics

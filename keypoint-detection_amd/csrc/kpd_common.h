@@ -74,4 +74,25 @@ __device__ __forceinline__ int split_a_exp(const float* sc_in, float maxb, float
   return min(max(14 - e, -100), 100);
 }
 
+// Split FPN level 0 computed by linearity (conv_glds.hip, fpn0x_kernel): the
+// stem tap and lateral 1 are split with their own power-of-two scales 2^a_f,
+// 2^a_l, chosen so that a_f + w_exp0 == a_l + w_expE == P (one unscale 2^-P
+// for the summed products) and neither operand overflows f16.  Whole-wave call.
+__device__ __forceinline__ int split_exp_of(float amax) {
+  const float u = amax * 1.0078125f;
+  if (!(u > 0.f)) return 100;   // all-zero tensor: no constraint
+  if (!(u < INFINITY)) return -100;
+  int e;
+  frexpf(u, &e);
+  return min(max(14 - e, -100), 100);
+}
+__device__ __forceinline__ void fpn0x_exps(const float* sc_in, int w_exp0, int w_expE, int* a_f, int* a_l, int* P) {
+  const int ef = split_exp_of(amax_read(sc_in)), el = split_exp_of(amax_read(sc_in + kAmaxSlots * kAmaxStride));
+  int pp = min(ef + w_exp0, el + w_expE);
+  pp = min(max(pp, -120), 120);
+  *P = pp;
+  *a_f = pp - w_exp0;
+  *a_l = pp - w_expE;
+}
+
 #define KPD_CHECK_LAUNCH() (hipGetLastError())

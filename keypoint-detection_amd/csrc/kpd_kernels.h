@@ -48,6 +48,32 @@ struct Conv16Args {
   int in_bytes, wt_bytes;   // filled by the launcher
 };
 hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st);
+
+// FPN level 0 by linearity (split mode): conv3x3(L0(tap0) + up4(lat1)) =
+// conv3x3'(tap0) [composite weights W3.L0, 16 input channels]
+// + per-position-class combinations of lat1 [taps summed by the lat1 pixel they
+// read after the exact 4x nearest upsample].  Output pixels are processed by
+// class (y % 4, x % 4), so every MFMA row of a tile uses the same weights.
+constexpr int kFpn0xMaxGroups = 4;
+struct Fpn0xArgs {
+  const void* f_split;     // tap0 as f16 [N][Hf][Wf][hi16 | lo16] (scale 2^a_f)
+  const void* l_split;     // lateral 1 as f16 [N][rh][rw][4 x (hi32 | lo32)] (scale 2^a_l)
+  const void* w0;          // [128][5 K-tiles][hi16(t) hi16(t+1) lo16(t) lo16(t+1)] (scale 2^w_exp0)
+  const void* weff;        // per class: [128][groups][4 chunks][hi32 | lo32] (scale 2^w_expE)
+  int cls_woff[16];        // f16-element offset of each class block in weff
+  int cls_ng[16];          // lat1 pixel groups of the class (1, 2 or 4)
+  int cls_g[16][kFpn0xMaxGroups];   // group g = (oy + 1) * 3 + (ox + 1)
+  const float* bias;       // [128] (fpn conv + BN, folded)
+  float* out;              // NHWC [N][Hf][Wf][128] fp32 (ReLU)
+  float* stats;            // [N][16 * tpc][2][128] channel sum / max per tile
+  const float* sc;         // amax slots: max|tap0|, max|lat1|
+  int N, Hf, Wf, rh, rw, tpc, w_exp0, w_expE;
+  int f_bytes, l_bytes, w0_bytes, weff_bytes;
+};
+hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
+// fp32 NHWC -> f16 hi|lo split rows (groups of 32 channels, or 16 for cin 16)
+hipError_t launch_split_rows(const float* in, long npix, int cin, const float* sc, int which, int w_exp0, int w_expE,
+                             void* out, hipStream_t st);
 int conv16_tile_m();
 
 enum ConvDType : int { CONV_F32 = 0, CONV_BF16_OUT_BF16 = 1, CONV_BF16_OUT_F32 = 2 };

@@ -167,6 +167,12 @@ struct kpd_plan {
     int w_exp = 0;
     float maxb = 0.f, maxs = 0.f;
   } fpn0s;  // split FPN level-0 weights
+  struct {
+    _Float16* w0 = nullptr;     // composite conv3x3.L0 weights [128][5][64]
+    _Float16* weff = nullptr;   // per position class [128][groups][4][64]
+    int w0_bytes = 0, weff_bytes = 0, w_exp0 = 0, w_expE = 0;
+    int cls_woff[16] = {}, cls_ng[16] = {}, cls_g[16][kFpn0xMaxGroups] = {};
+  } fpn0x;  // FPN level 0 by linearity (conv_glds.hip, fpn0x_kernel)
   float *fin_w = nullptr, *fin_b = nullptr;
   float* zero_bias = nullptr;  // 128 zeros for bias-free laterals
   // person-detector glue: box_heads[0] ++ cls_heads[0] as one 1x1 conv (45 -> 48 ch)
@@ -380,6 +386,104 @@ int pack_split16(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
   return KPD_OK;
 }
 
+// FPN level 0 by linearity (fpn0x_kernel): W0 = W3 . L0 (the 3x3 conv on the
+// 16-channel stem tap through the bias-free lateral 0) and, per output position
+// class (y % 4, x % 4), the 3x3 taps summed by the lateral-1 pixel they read
+// after the exact 4x nearest upsample.  Products in double; split into f16
+// hi + lo after a power-of-two scale (one per weight set).
+int pack_fpn0x(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
+  if (dc.cin_p != 128 || dc.cout_p != 128 || lat0.cin_p != 16 || lat0.cout_p != 128) return KPD_OK;   // path unused
+  const size_t n3 = (size_t)128 * 9 * 128;
+  std::vector<float> w3(n3), l0((size_t)128 * 16);
+  HIP_TRY(hipMemcpy(w3.data(), dc.w, n3 * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(l0.data(), lat0.w, l0.size() * sizeof(float), hipMemcpyDeviceToHost));
+  auto W3 = [&](int co, int t, int k) { return (double)w3[((size_t)co * 9 + t) * 128 + k]; };
+  // composite tap0 weights [co][t][c]
+  std::vector<double> w0((size_t)128 * 9 * 16, 0.0);
+  double m0 = 0.0;
+  for (int co = 0; co < 128; ++co)
+    for (int t = 0; t < 9; ++t)
+      for (int c = 0; c < 16; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < 128; ++k) acc += W3(co, t, k) * (double)l0[(size_t)k * 16 + c];
+        w0[((size_t)co * 9 + t) * 16 + c] = acc;
+        m0 = std::max(m0, std::fabs(acc));
+      }
+  // per class: tap groups by lateral-1 pixel offset
+  auto off = [](int a, int d) { return a + d < 0 ? -1 : (a + d > 3 ? 1 : 0); };
+  std::vector<double> weff;
+  double mE = 0.0;
+  int woff = 0;
+  for (int cls = 0; cls < 16; ++cls) {
+    const int a = cls >> 2, b = cls & 3;
+    int gid[9], ng = 0;
+    for (int t = 0; t < 9; ++t) {
+      const int gg = (off(a, t / 3 - 1) + 1) * 3 + (off(b, t % 3 - 1) + 1);
+      int g = 0;
+      while (g < ng && p->fpn0x.cls_g[cls][g] != gg) ++g;
+      if (g == ng) {
+        if (ng == kFpn0xMaxGroups) return fail(KPD_ESTATE, "fpn0x: more than 4 tap groups");
+        p->fpn0x.cls_g[cls][ng++] = gg;
+      }
+      gid[t] = g;
+    }
+    p->fpn0x.cls_ng[cls] = ng;
+    p->fpn0x.cls_woff[cls] = woff;
+    std::vector<double> blk((size_t)128 * ng * 128, 0.0);   // [co][g][k]
+    for (int co = 0; co < 128; ++co)
+      for (int t = 0; t < 9; ++t)
+        for (int k = 0; k < 128; ++k) blk[((size_t)co * ng + gid[t]) * 128 + k] += W3(co, t, k);
+    for (double v : blk) mE = std::max(mE, std::fabs(v));
+    weff.insert(weff.end(), blk.begin(), blk.end());
+    woff += 128 * ng * 128 * 2;   // f16 elements (hi + lo)
+  }
+  auto wexp = [](double m) {
+    int e = 0;
+    if (m > 0.0) std::frexp(m, &e);
+    return std::min(std::max(14 - e, -100), 100);
+  };
+  const int e0 = wexp(m0), eE = wexp(mE);
+  auto split = [](double x, _Float16* hi, _Float16* lo) {
+    *hi = (_Float16)x;
+    *lo = (_Float16)(x - (double)*hi);
+  };
+  // W0 rows [co][kt][hi16(2kt) hi16(2kt+1) lo16(2kt) lo16(2kt+1)], tap 9 = zero
+  std::vector<_Float16> h0((size_t)128 * 5 * 64, (_Float16)0.f);
+  for (int co = 0; co < 128; ++co)
+    for (int t = 0; t < 9; ++t)
+      for (int c = 0; c < 16; ++c) {
+        _Float16 hi, lo;
+        split(std::ldexp(w0[((size_t)co * 9 + t) * 16 + c], e0), &hi, &lo);
+        const size_t row = ((size_t)co * 5 + t / 2) * 64, sub = (t & 1) * 16 + c;
+        h0[row + sub] = hi;
+        h0[row + 32 + sub] = lo;
+      }
+  // W_eff rows [co][g][kc][hi32 | lo32]
+  std::vector<_Float16> hE((size_t)woff, (_Float16)0.f);
+  size_t src = 0;
+  for (int cls = 0; cls < 16; ++cls) {
+    const int ng = p->fpn0x.cls_ng[cls];
+    _Float16* dst = hE.data() + p->fpn0x.cls_woff[cls];
+    for (int co = 0; co < 128; ++co)
+      for (int g = 0; g < ng; ++g)
+        for (int k = 0; k < 128; ++k) {
+          _Float16 hi, lo;
+          split(std::ldexp(weff[src + ((size_t)co * ng + g) * 128 + k], eE), &hi, &lo);
+          const size_t row = (((size_t)co * ng + g) * 4 + k / 32) * 64;
+          dst[row + k % 32] = hi;
+          dst[row + 32 + k % 32] = lo;
+        }
+    src += (size_t)128 * ng * 128;
+  }
+  if (int rc = upload(p, h0, &p->fpn0x.w0)) return rc;
+  if (int rc = upload(p, hE, &p->fpn0x.weff)) return rc;
+  p->fpn0x.w0_bytes = (int)(h0.size() * 2);
+  p->fpn0x.weff_bytes = (int)(hE.size() * 2);
+  p->fpn0x.w_exp0 = e0;
+  p->fpn0x.w_expE = eE;
+  return KPD_OK;
+}
+
 // ------------------------------------------------------------------ workspace
 constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
 constexpr int kFuseMaxPix = 16 * 12;        // input maps up to this size take the fused expand+depthwise
@@ -587,6 +691,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   for (void* a : p->allocs) (void)hipFree(a);
   p->allocs.clear();
   p->fpn0s.hl = nullptr;
+  p->fpn0x.w0 = p->fpn0x.weff = nullptr;
   p->pd = DevConv();
   p->anchors = nullptr;
   p->kh_ds1 = DevConv();
@@ -653,7 +758,10 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
-  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_split16(p, p->fpn0, p->lat[0]));
+  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) {
+    chk(pack_split16(p, p->fpn0, p->lat[0]));
+    chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
+  }
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
@@ -788,8 +896,13 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   d.Hf = d.h[0]; d.Wf = d.w[0];
   const bool split = p->precision == KPD_PRECISION_MIXED && p->fpn0s.hl != nullptr;
   const int HWf = d.Hf * d.Wf, TM = split ? conv16_tile_m() : conv_tile_m();
-  d.fused_stats = (HWf % TM) == 0;
-  d.tiles = d.fused_stats ? HWf / TM : std::min(64, HWf);
+  // FPN level 0 by linearity when lateral 1 is an exact 4x nearest upsample
+  static const bool no_lin = getenv("KPD_NO_FPN0X") != nullptr;   // A/B switch
+  const bool lin = split && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] && d.Wf == 4 * d.w[3] &&
+                   (size_t)B * HWf * 64 < 0x7fffffffu;   // 31-bit buffer descriptors
+  const int tpc = (d.h[3] * d.w[3] + 255) / 256;   // fpn0x tiles per (position class, image)
+  d.fused_stats = lin || (HWf % TM) == 0;
+  d.tiles = lin ? 16 * tpc : (d.fused_stats ? HWf / TM : std::min(64, HWf));
   if (int rc = ensure_work(p, d, k, st)) return rc;
   Work& w = p->work[k];
   g_splitk = w.splitk;
@@ -878,6 +991,14 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   for (int i = 3; i >= 0; --i) {
     const DevConv& L = p->lat[i];
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
+    if (i == 0 && lin) {   // no lateral 0: tap0 and lateral 1 go to the split layouts fpn0x_kernel reads
+      char* base = reinterpret_cast<char*>(w.lat[0]);
+      HIP_TRY(launch_split_rows(taps[0], (long)B * lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
+                                base, st));
+      HIP_TRY(launch_split_rows(w.lat[1], (long)B * lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
+                                p->fpn0x.w_expE, base + (size_t)B * lh[0] * lw[0] * 64, st));
+      continue;
+    }
     if (i == 0 && L.cin_p <= 32) {   // the 16-channel stem tap: a 403 MB/step stream, not a GEMM
       HIP_TRY(launch_lateral_stream(taps[0], L.cin_p, (const float*)L.w, L.b, res, B, lh[0], lw[0], lh[1], lw[1],
                                     w.lat[0], nullptr, split ? w.sc : nullptr, p->fpn0s.maxb, p->fpn0s.maxs, st));
@@ -891,7 +1012,25 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   }
   lat_stage.reset();
   std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
-  if (split) {
+  if (lin) {
+    Fpn0xArgs a{};
+    char* base = reinterpret_cast<char*>(w.lat[0]);
+    a.f_split = base;
+    a.l_split = base + (size_t)B * lh[0] * lw[0] * 64;
+    a.w0 = p->fpn0x.w0; a.weff = p->fpn0x.weff;
+    for (int c = 0; c < 16; ++c) {
+      a.cls_woff[c] = p->fpn0x.cls_woff[c];
+      a.cls_ng[c] = p->fpn0x.cls_ng[c];
+      for (int g = 0; g < kFpn0xMaxGroups; ++g) a.cls_g[c][g] = p->fpn0x.cls_g[c][g];
+    }
+    a.bias = p->fpn0.b; a.out = w.feat; a.stats = w.stats; a.sc = w.sc;
+    a.N = B; a.Hf = d.Hf; a.Wf = d.Wf; a.rh = lh[1]; a.rw = lw[1]; a.tpc = tpc;
+    a.w_exp0 = p->fpn0x.w_exp0; a.w_expE = p->fpn0x.w_expE;
+    a.f_bytes = (int)std::min<size_t>((size_t)B * lh[0] * lw[0] * 64, 0x7fffffff);
+    a.l_bytes = (int)std::min<size_t>((size_t)B * lh[1] * lw[1] * 512, 0x7fffffff);
+    a.w0_bytes = p->fpn0x.w0_bytes; a.weff_bytes = p->fpn0x.weff_bytes;
+    HIP_TRY(launch_fpn0x(a, st));
+  } else if (split) {
     Conv16Args a{};
     a.in = w.lat[0]; a.wt = p->fpn0s.hl; a.bias = p->fpn0.b; a.out = w.feat;
     a.stats = d.fused_stats ? w.stats : nullptr;
