@@ -38,20 +38,32 @@ def conv_flops(cin, cout, k, h, w, groups=1):
     return 2.0 * cout * (cin // groups) * k * k * h * w
 
 
+# torchvision mobilenet_v3_small features.1-11 rows (in, k, exp, out, SE, act,
+# stride) -- the architecture table, used here only to count FLOPs
+BNECK = ((16, 3, 16, 16, True, "RE", 2), (16, 3, 72, 24, False, "RE", 2), (24, 3, 88, 24, False, "RE", 1),
+         (24, 5, 96, 40, True, "HS", 2), (40, 5, 240, 40, True, "HS", 1), (40, 5, 240, 40, True, "HS", 1),
+         (40, 5, 120, 48, True, "HS", 1), (48, 5, 144, 48, True, "HS", 1), (48, 5, 288, 96, True, "HS", 2),
+         (96, 5, 576, 96, True, "HS", 1), (96, 5, 576, 96, True, "HS", 1))
+
+
+def _make_divisible(v, d=8):
+    n = max(d, int(v + d / 2) // d * d)
+    return n + d if n < 0.9 * v else n
+
+
 def flops_per_image(H, W, P, in_ch=3):
     """Algorithmic FLOPs (2*MAC of conv/linear, BN folded, dead FPN levels 1-3
     excluded) -- SURVEY.md §8(d)."""
-    from oracle.kpd_oracle import MBV3_SMALL_BNECK, make_divisible
     h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     f = conv_flops(in_ch, 16, 3, h, w)
     sizes = [(h, w)]
-    for cin, k, exp, cout, se, _a, s in MBV3_SMALL_BNECK:
+    for cin, k, exp, cout, se, _a, s in BNECK:
         if exp != cin:
             f += conv_flops(cin, exp, 1, h, w)
         ho, wo = (h + 2 * ((k - 1) // 2) - k) // s + 1, (w + 2 * ((k - 1) // 2) - k) // s + 1
         f += conv_flops(exp, exp, k, ho, wo, groups=exp)
         if se:
-            sq = make_divisible(exp // 4, 8)
+            sq = _make_divisible(exp // 4, 8)
             f += 2.0 * (exp * sq * 2)
         f += conv_flops(exp, cout, 1, ho, wo)
         h, w = ho, wo
@@ -192,7 +204,21 @@ def main():
     n_sub = max(1, min(a.streams, 4, B // 16))
     Bl = B
     # (label, peak TFLOP/s for the ALGORITHMIC flops, kernel description)
+    # mixed precision with an exact 4x lateral-1 upsample runs FPN level 0 by
+    # linearity (fpn0x_kernel): the ALGORITHMIC flops stay those of the 3x3
+    # conv over lateral 0; the MFMA work actually issued is
+    # reported beside them (executed_*)
+    hf, wf = (a.height - 1) // 2 + 1, (a.width - 1) // 2 + 1
+    h1, w1 = hf, wf
+    for _cin, k, _e, _co, _se, _a, st in BNECK[:3]:
+        pd = (k - 1) // 2
+        h1, w1 = (h1 + 2 * pd - k) // st + 1, (w1 + 2 * pd - k) // st + 1
+    lin = mixed and hf == 4 * h1 and wf == 4 * w1
+    exec_fpn0 = (2.0 * hf * wf * (5 * 32 * 128 + 36 * 128 * 128 / 16) * Bl) if lin else None
     mfma = {"fpn0": (fl["fpn0"] * Bl, PEAK_TFLOPS["bf16"] / 3.0 if mixed else PEAK_TFLOPS["fp32"],
+                     ("fpn0 conv3x3 128->128 by linearity (composite 16-ch 3x3 on the stem tap + per-position-class "
+                      "lateral-1 tap groups), fp32-accurate 3-product f16 split on v_mfma_f32_16x16x32_f16 "
+                      "(peak = 2500/3 TF/s fp32-equivalent)") if lin else
                      "fpn0 conv3x3 128->128: fp32-accurate 3-product f16 split on v_mfma_f32_16x16x32_f16 "
                      "(peak = 2500/3 TF/s fp32-equivalent)" if mixed else
                      "fpn0 conv3x3 128->128 on v_mfma_f32_16x16x4_f32")}
@@ -217,6 +243,10 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                 "traffic_unit": "bytes/launch (rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE)",
                 "flop_per_launch": flop, "avg_ms": round(stages[dom], 4)}
+        if dom == "fpn0" and exec_fpn0:
+            ex = exec_fpn0 / (stages[dom] * 1e-3) / 1e12
+            roof.update({"executed_flop_per_launch": exec_fpn0, "executed_achieved": round(ex, 2),
+                         "executed_frac": round(ex / peak, 4)})
 
     total_imgs = B * world * a.steps
     line = {
