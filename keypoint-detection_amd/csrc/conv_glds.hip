@@ -441,9 +441,11 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int Hf = p.Hf, Wf = p.Wf, rh = p.rh, rw = p.rw, RG = rh * rw;
-  const int per_cls = p.N * p.tpc;
+  // tile order: position class fastest, so the 16 classes of one (image, row
+  // block) -- which read the same tap0 / lateral-1 pixels -- run back to back
+  // on one XCD (xcd_remap) and share its L2
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int cls = L / per_cls, rem = L - cls * per_cls, n = rem / p.tpc, jt = rem - n * p.tpc;
+  const int cls = L & 15, nj = L >> 4, n = nj / p.tpc, jt = nj - n * p.tpc;
   const int ca = cls >> 2, cb = cls & 3;
   const int q0 = jt * BM;                         // first lat1-grid pixel of the tile
   const int NG = p.cls_ng[cls];
