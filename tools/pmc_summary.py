@@ -17,7 +17,8 @@ from collections import defaultdict
 
 STAGE_OF = {   # kernel-name substring -> "<stage>:<bench precision>"
     "conv_mfma_kernel<float, float, 3, 128, 128, 32": "fpn0:fp32",
-    "conv16_kernel<true": "fpn0:mixed",
+    "conv16_kernel<true": "fpn0:mixed",       # direct 3x3 over lateral 0 (KPD_NO_FPN0X=1)
+    "fpn0x_kernel": "fpn0:mixed",             # FPN level 0 by linearity (default)
 }
 
 
