@@ -18,6 +18,16 @@
 
 namespace {
 
+constexpr int kSeExcitePart = 6144;   // fc1 partial floats per image staged by se_excite_kernel
+
+// In-kernel phase stamps (diagnostic, KPD_STAMPS): thread 0 of each workgroup
+// records s_memrealtime (100 MHz) at phase boundaries into its own 8-slot row
+// of a buffer no other code reads.
+__device__ __forceinline__ void stamp(unsigned long long* st, int i) {
+  if (st && threadIdx.x == 0)
+    st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
 // Stem: 3x3 stride-2 conv (CIN -> 16) + folded BN + h-swish, NCHW image in,
 // NHWC out; CIN is a template argument so the 9*CIN inputs stay in registers.
 template <int CIN>
@@ -215,86 +225,131 @@ __device__ __forceinline__ void se_fc(const float* mean, float* hid, int nimg, i
 
 // Fused MobileNetV3 inverted-residual front half for the coarse maps:
 // expand 1x1 (+ folded BN + act) -> depthwise KxK stride S (+ folded BN + act)
-// -> output, plus the per-image channel means the SE block needs.  One
-// workgroup per (image, slice of CS expanded channels): the whole input image
-// is staged in LDS once, the expanded slice never leaves LDS (no HBM round
-// trip, one launch instead of two, and the SE pooling pass disappears).  The
-// depthwise zero padding is the LDS image's border test.  Channel means are
-// reduced in a fixed order (deterministic).  torchvision InvertedResidual
-// (backbone.py:250-254 via mobilenet_v3_small).
-template <int K, int S>
+// -> output, plus the per-image channel means the SE block needs and, when
+// p.part is set, the SE fc1 partial products of this slice's channels
+// (fc1 is linear in the means, so fc1(mean) = sum over slices of
+// w1[:, slice] . mean[slice]; seproj_kernel finishes it).  One workgroup per
+// (image, slice of CS = 16 * NTC expanded channels).  torchvision
+// InvertedResidual (backbone.py:250-254 via mobilenet_v3_small).
+//   * every weight / input load of a phase is issued before its first use
+//     (register batches): the phases are latency chains, not throughput;
+//   * expand on v_mfma_f32_16x16x4_f32 (exact fp32 products): A = 16 input
+//     pixels x 16 channels of x straight from L2 (16 bytes per lane), B = the
+//     slice's expand weights, kept in registers for all M tiles;
+//   * the expanded slice lives in LDS only, rows padded to CS + 4 floats so the
+//     depthwise's 16-byte reads of 4 column groups hit distinct banks;
+//   * channel means reduced in a fixed order (deterministic, batch-independent).
+template <int K, int S, int NTC, int XT, int KC>
 __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int n = blockIdx.y, c0 = blockIdx.x * p.CS, tid = threadIdx.x;
-  const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, CS = p.CS, cq = CS / 4, cin_p = p.cin_p;
-  // LDS: [weT: cin_p x CS] [es: Pin x CS] [wds: K*K x CS] [ds: Po x CS, the means]
-  float* weT = sm;
-  float* es = weT + (p.we ? cin_p * CS : 0);
-  float* wds = es + Pin * CS;
-  float* ds = wds + K * K * CS;
+  // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
+  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = CS + 4, DA = KC <= 3 ? 4 : 2;
+  const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, cin_p = p.cin_p;
+  float* es = sm;                                  // [Pin][ESTR]
+  float* wds = es + Pin * ESTR;                    // [K*K][CS]
+  float* ds = wds + K * K * CS;                    // [Po][CS] (pooled)
+  float* w1s = ds + (p.pooled ? Po * CS : 0);      // [sq][CS] (part)
   const float* xg = p.x + (size_t)n * Pin * cin_p;
-  if (p.we) {
-    for (int i = tid; i < cin_p * CS; i += 256) {   // transposed weight slice: weT[k][c]
-      const int c = i / cin_p, k = i - c * cin_p;
-      weT[k * CS + c] = p.we[(size_t)(c0 + c) * cin_p + k];
+  stamp(p.stamps, 0);
+  const int r = lane & 15, g = lane >> 4;
+  const int nmt = (Pin + 15) / 16, ntw = (nmt - wave + 3) / 4;   // M tiles of this wave: wave + 4 t
+  // one round trip for everything the expand needs: B fragments (all k
+  // chunks, all N tiles) and the first DA M tiles' A fragments -> registers,
+  // then the depthwise weights and the fc1 columns -> LDS
+  float4 bw[NTC][KC];
+#pragma unroll
+  for (int nt = 0; nt < NTC; ++nt)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      bw[nt][kc] = *reinterpret_cast<const float4*>(p.we + (size_t)(c0 + nt * 16 + r) * cin_p + kc * 16 + g * 4);
+  float4 av[DA][KC];
+  auto load_a = [&](int t, float4* a4) {
+    if (t < ntw) {
+      const int px = min((wave + 4 * t) * 16 + r, Pin - 1);
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) a4[kc] = *reinterpret_cast<const float4*>(xg + (size_t)px * cin_p + kc * 16 + g * 4);
     }
-  } else {   // no expand (exp == cin): the slice of x is the depthwise input
-    for (int i = tid; i < Pin * cq; i += 256) {
-      const int px = i / cq, q = i - px * cq;
-      reinterpret_cast<float4*>(es)[i] = *reinterpret_cast<const float4*>(xg + (size_t)px * cin_p + c0 + q * 4);
+  };
+#pragma unroll
+  for (int d = 0; d < DA; ++d) load_a(d, av[d]);
+  {
+    constexpr int NW = (K * K * CQ + 255) / 256;
+    float4 v[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int i = tid + u * 256, t = i / CQ, q = i - t * CQ;
+      if (i < K * K * CQ) v[u] = *reinterpret_cast<const float4*>(p.wd + (size_t)t * p.Ep + c0 + q * 4);
+    }
+    constexpr int NJ = (144 * CQ + 255) / 256;   // sq <= 144 (launch check)
+    float4 v1[NJ];
+    if (p.part) {
+#pragma unroll
+      for (int u = 0; u < NJ; ++u) {
+        const int i = tid + u * 256, j = i / CQ, q = i - j * CQ;
+        v1[u] = (i < p.sq * CQ && c0 + q * 4 < p.C)
+                    ? *reinterpret_cast<const float4*>(p.w1 + (size_t)j * p.C + c0 + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int i = tid + u * 256;
+      if (i < K * K * CQ) reinterpret_cast<float4*>(wds)[i] = v[u];
+    }
+    if (p.part) {
+#pragma unroll
+      for (int u = 0; u < NJ; ++u) {
+        const int i = tid + u * 256;
+        if (i < p.sq * CQ) reinterpret_cast<float4*>(w1s)[i] = v1[u];
+      }
     }
   }
-  for (int i = tid; i < K * K * cq; i += 256) {
-    const int t = i / cq, q = i - t * cq;
-    reinterpret_cast<float4*>(wds)[i] = *reinterpret_cast<const float4*>(p.wd + (size_t)t * p.Ep + c0 + q * 4);
-  }
-  __syncthreads();
-  if (p.we) {
-    // expand, register-tiled 4 pixels x 4 channels: x rows straight from
-    // global/L1 (shared by the slice's cq threads), weights from LDS
-    const int pg_n = (Pin + 3) / 4;
-    for (int i = tid; i < pg_n * cq; i += 256) {
-      const int pg = i / cq, q = i - pg * cq;
-      const float4 b = *reinterpret_cast<const float4*>(p.be + c0 + q * 4);
-      float a[4][4];
+  stamp(p.stamps, 1);
+  // expand: DA M tiles of A in flight per wave; a tile's slot is refilled
+  // with the tile DA ahead right after its MFMAs
+  {
+    float be[NTC];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { a[r][0] = b.x; a[r][1] = b.y; a[r][2] = b.z; a[r][3] = b.w; }
-      const float* xr[4];
+    for (int nt = 0; nt < NTC; ++nt) be[nt] = p.be[c0 + nt * 16 + r];
+    for (int t0 = 0; t0 < ntw; t0 += DA) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) xr[r] = xg + (size_t)min(pg * 4 + r, Pin - 1) * cin_p;
-      for (int k = 0; k < cin_p; k += 4) {
-        float4 xv[4], wv[4];
+      for (int d = 0; d < DA; ++d) {
+        const int t = t0 + d;
+        if (t < ntw) {
+          f32x4 acc[NTC];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4*>(xr[r] + k);
+          for (int nt = 0; nt < NTC; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wv[j] = *reinterpret_cast<const float4*>(weT + (k + j) * CS + q * 4);
+          for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float xs[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
+            for (int nt = 0; nt < NTC; ++nt) {
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].x, bw[nt][kc].x, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].y, bw[nt][kc].y, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].z, bw[nt][kc].z, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].w, bw[nt][kc].w, acc[nt], 0, 0, 0);
+            }
+          load_a(t + DA, av[d]);
+          // C layout: col = lane & 15 (channel), row = 4 * (lane >> 4) + i (pixel)
+          const int mt = wave + 4 * t;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            a[r][0] = fmaf(xs[j], wv[j].x, a[r][0]); a[r][1] = fmaf(xs[j], wv[j].y, a[r][1]);
-            a[r][2] = fmaf(xs[j], wv[j].z, a[r][2]); a[r][3] = fmaf(xs[j], wv[j].w, a[r][3]);
-          }
+          for (int nt = 0; nt < NTC; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int px = mt * 16 + g * 4 + i;
+              if (px < Pin) es[px * ESTR + nt * 16 + r] = kpd_act(acc[nt][i] + be[nt], p.act_e);
+            }
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int px = pg * 4 + r;
-        if (px < Pin)
-          reinterpret_cast<float4*>(es)[px * cq + q] =
-              make_float4(kpd_act(a[r][0], p.act_e), kpd_act(a[r][1], p.act_e), kpd_act(a[r][2], p.act_e),
-                          kpd_act(a[r][3], p.act_e));
-      }
     }
-    __syncthreads();
   }
-  // depthwise from LDS, 4 consecutive output columns per thread (input columns
-  // reused from registers as in dwconv_kernel)
-  constexpr int PD = (K - 1) / 2, XT = 4, NC = (XT - 1) * S + K;
+  __syncthreads();
+  stamp(p.stamps, 2);
+  // depthwise from LDS, XT consecutive output columns per thread (input
+  // columns reused from registers as in dwconv_kernel)
+  constexpr int PD = (K - 1) / 2, NC = (XT - 1) * S + K;
   const int wx = (p.Wo + XT - 1) / XT;
-  for (int i = tid; i < p.Ho * wx * cq; i += 256) {
-    const int q = i % cq, r = i / cq, xt = r % wx, oy = r / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
+  for (int i = tid; i < p.Ho * wx * CQ; i += 256) {
+    const int q = i % CQ, rr = i / CQ, xt = rr % wx, oy = rr / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
     float4 a[XT];
 #pragma unroll
     for (int o = 0; o < XT; ++o) a[o] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -306,12 +361,12 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int ix = ix0 + c;
-        col[c] = (ix >= 0 && ix < p.Wi) ? reinterpret_cast<const float4*>(es)[(iy * p.Wi + ix) * cq + q]
+        col[c] = (ix >= 0 && ix < p.Wi) ? *reinterpret_cast<const float4*>(es + (iy * p.Wi + ix) * ESTR + q * 4)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int kx = 0; kx < K; ++kx) {
-        const float4 w = reinterpret_cast<const float4*>(wds)[(ky * K + kx) * cq + q];
+        const float4 w = reinterpret_cast<const float4*>(wds)[(ky * K + kx) * CQ + q];
 #pragma unroll
         for (int o = 0; o < XT; ++o) {
           const float4 v = col[o * S + kx];
@@ -329,23 +384,268 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       v.z = kpd_act(a[o].z + b.z, p.act_d); v.w = kpd_act(a[o].w + b.w, p.act_d);
       const int op = oy * p.Wo + ox0 + o;
       *reinterpret_cast<float4*>(p.out + ((size_t)n * Po + op) * p.Ep + c0 + q * 4) = v;
-      if (p.pooled) reinterpret_cast<float4*>(ds)[op * cq + q] = v;
+      if (p.pooled) reinterpret_cast<float4*>(ds)[op * CQ + q] = v;
     }
   }
   if (p.pooled) {   // channel means: 256/CS row groups in parallel, then a fixed-order combine
     __syncthreads();
-    const int groups = 256 / CS, c = tid % CS, g = tid / CS;
+    stamp(p.stamps, 3);
+    constexpr int groups = 256 / CS;
+    const int c = tid % CS, gg0 = tid / CS;
     float sum = 0.f;
-    if (g < groups)
-      for (int op = g; op < Po; op += groups) sum += ds[op * CS + c];
+    for (int op = gg0; op < Po; op += groups) sum += ds[op * CS + c];
     __syncthreads();
-    if (g < groups) ds[g * CS + c] = sum;
+    ds[gg0 * CS + c] = sum;
     __syncthreads();
     if (tid < CS) {
       float t = 0.f;
+#pragma unroll
       for (int gg = 0; gg < groups; ++gg) t += ds[gg * CS + tid];
-      p.pooled[(size_t)n * p.Ep + c0 + tid] = t / (float)Po;
+      t /= (float)Po;
+      p.pooled[(size_t)n * p.Ep + c0 + tid] = t;
+      ds[tid] = t;   // column tid of ds is read only by this thread above
     }
+    if (p.part) {   // SE fc1 partial of this slice, one output row per thread
+      __syncthreads();
+      const int nsl = gridDim.x;
+      for (int j = tid; j < p.sq; j += 256) {
+        float acc = 0.f;
+#pragma unroll
+        for (int c2 = 0; c2 < CS; ++c2) acc = fmaf(w1s[j * CS + c2], ds[c2], acc);
+        p.part[((size_t)n * nsl + blockIdx.x) * p.sq + j] = acc;
+      }
+    }
+  }
+  stamp(p.stamps, 4);
+}
+
+// Squeeze-excitation excitation + project 1x1 (+ residual) for the coarse
+// maps (features.4..11 of mobilenet_v3_small; torchvision SqueezeExcitation +
+// InvertedResidual, backbone.py:250-254).  One workgroup per (image, NTT*16
+// output channels):
+//   hid = ReLU(b1 + sum over slices of exdw_kernel's fc1 partials)  (fixed order)
+//   s   = hardsigmoid(b2 + W2 . hid)                                  (all Ep channels, LDS)
+//   out = (d * s) . Wp^T + bp (+ x)
+// (with a.sesc set, s comes precomputed from se_excite_kernel instead).
+// The project GEMM runs on v_mfma_f32_16x16x4_f32 (exact fp32 products): each
+// lane loads 16 bytes of a d row and of a Wp row per 16-wide k chunk and feeds
+// them to 4 MFMAs (k-step t takes element t; A and B use the same k
+// permutation).  The 4 waves split the k chunks; their partial tiles are summed
+// in LDS in wave order (deterministic, independent of the batch).  The first
+// D chunks' loads do not depend on s and are issued before the excitation, so
+// their latency hides under it; each chunk's slot is refilled D chunks ahead.
+template <int MT, int NTT>
+__global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int NT = NTT * 16, MP = MT * 16;
+  constexpr int D = (28 / (MT + NTT)) < 1 ? 1 : ((28 / (MT + NTT)) > 4 ? 4 : 28 / (MT + NTT));
+  const int n = blockIdx.y, o0 = blockIdx.x * NT, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Ep = a.Ep, Po = a.Po;
+  float* sS = sm;                    // [Ep] excitation
+  float* hid = sS + Ep;              // [256]
+  float* red = hid + 256;            // [4][MP][NT] partial tiles / SE scratch
+  stamp(a.stamps, 0);
+  const int r = lane & 15, g = lane >> 4;
+  const float* dbase = a.d + (size_t)n * Po * Ep;
+  const int nkc = Ep / 16, ncw = (nkc - wave + 3) / 4;   // this wave's k chunks: wave + 4 t
+  float4 av[D][MT], bv[D][NTT];
+  auto load_chunk = [&](int t, float4* a4, float4* b4) {
+    if (t < ncw) {
+      const int k = (wave + 4 * t) * 16 + g * 4;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int px = mt * 16 + r;
+        a4[mt] = px < Po ? *reinterpret_cast<const float4*>(dbase + (size_t)px * Ep + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NTT; ++nt) b4[nt] = *reinterpret_cast<const float4*>(a.wp + (size_t)(o0 + nt * 16 + r) * Ep + k);
+    }
+  };
+#pragma unroll
+  for (int dd = 0; dd < D; ++dd) load_chunk(dd, av[dd], bv[dd]);
+  if (a.sesc) {   // precomputed excitation
+    for (int c = tid; c < Ep / 4; c += 256)
+      reinterpret_cast<float4*>(sS)[c] = reinterpret_cast<const float4*>(a.sesc + (size_t)n * Ep)[c];
+    __syncthreads();
+  } else {
+    // (1) hid = ReLU(b1 + sum of the slice partials): the image's partials
+    // staged in LDS first (all loads in flight), then summed in slice order
+    const int npart = a.nsl * a.sq;
+    const float* part = a.part + (size_t)n * npart;
+    {
+      constexpr int NP = 6;   // npart / 4 <= 1536 (kSePartFloats / 4 / ... checked at launch)
+      float4 v[NP];
+#pragma unroll
+      for (int u = 0; u < NP; ++u)   // clamped (unconditional) loads keep v in registers
+        v[u] = reinterpret_cast<const float4*>(part)[min(tid + u * 256, npart / 4 - 1)];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int i = tid + u * 256;
+        if (i < npart / 4) reinterpret_cast<float4*>(red)[i] = v[u];
+      }
+    }
+    __syncthreads();
+    for (int j = tid; j < a.sq; j += 256) {
+      float h = 0.f;
+      for (int s2 = 0; s2 < a.nsl; ++s2) h += red[s2 * a.sq + j];
+      hid[j] = fmaxf(h + a.b1[j], 0.f);
+    }
+    __syncthreads();
+    stamp(a.stamps, 1);
+    // (2) s = hardsigmoid(b2 + W2 . hid), W2 transposed [sq][C]: a work item is
+    // (channel quad, j group); the group's rows are loaded together (16-byte
+    // loads), the j groups' partial sums meet in LDS in group order
+    {
+      const int nq4 = a.C / 4, ngrp = max(1, min(16, 256 / nq4)), items = nq4 * ngrp;
+      const int jper = (a.sq + ngrp - 1) / ngrp;
+      float* fsum = red;   // [ngrp][C]
+      for (int it = tid; it < items; it += 256) {
+        const int q = it % nq4, gi = it / nq4, j0 = gi * jper, j1 = min(a.sq, j0 + jper);
+        float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        constexpr int JU = 16;
+        for (int j = j0; j < j1; j += JU) {
+          float4 wv[JU];
+#pragma unroll
+          for (int u = 0; u < JU; ++u)
+            if (j + u < j1) wv[u] = *reinterpret_cast<const float4*>(a.w2t + (size_t)(j + u) * a.C + q * 4);
+#pragma unroll
+          for (int u = 0; u < JU; ++u)
+            if (j + u < j1) {
+              const float h = hid[j + u];
+              acc4.x = fmaf(wv[u].x, h, acc4.x); acc4.y = fmaf(wv[u].y, h, acc4.y);
+              acc4.z = fmaf(wv[u].z, h, acc4.z); acc4.w = fmaf(wv[u].w, h, acc4.w);
+            }
+        }
+        reinterpret_cast<float4*>(fsum + (size_t)gi * a.C)[q] = acc4;
+      }
+      __syncthreads();
+      for (int c = tid; c < Ep; c += 256) {
+        float t = 0.f;
+        if (c < a.C)
+          for (int gi = 0; gi < ngrp; ++gi) t += fsum[(size_t)gi * a.C + c];
+        sS[c] = c < a.C ? kpd_hsigmoid(t + a.b2[c]) : 0.f;
+      }
+      __syncthreads();
+    }
+  }
+  stamp(a.stamps, 2);
+  // (3) project on MFMA
+  f32x4 acc[MT][NTT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t0 = 0; t0 < ncw; t0 += D) {
+#pragma unroll
+    for (int dd = 0; dd < D; ++dd) {
+      const int t = t0 + dd;
+      if (t < ncw) {
+        const float4 sv = *reinterpret_cast<const float4*>(sS + (wave + 4 * t) * 16 + g * 4);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float4 x4 = make_float4(av[dd][mt].x * sv.x, av[dd][mt].y * sv.y, av[dd][mt].z * sv.z,
+                                        av[dd][mt].w * sv.w);
+#pragma unroll
+          for (int nt = 0; nt < NTT; ++nt) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(x4.x, bv[dd][nt].x, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(x4.y, bv[dd][nt].y, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(x4.z, bv[dd][nt].z, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(x4.w, bv[dd][nt].w, acc[mt][nt], 0, 0, 0);
+          }
+        }
+        load_chunk(t + D, av[dd], bv[dd]);
+      }
+    }
+  }
+  __syncthreads();   // (red held the SE scratch)
+  // partial tiles -> LDS (C layout: col = lane & 15, row = 4 * (lane >> 4) + i)
+  float* rw = red + (size_t)wave * MP * NT;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rw[(mt * 16 + g * 4 + i) * NT + nt * 16 + r] = acc[mt][nt][i];
+  __syncthreads();
+  stamp(a.stamps, 3);
+  // (4) sum the 4 waves in order, bias, residual; 4 channels per thread
+  constexpr int NQ = NT / 4;
+  float* out = a.out + (size_t)n * Po * a.cout_p + o0;
+  const float* res = a.res ? a.res + (size_t)n * Po * a.cout_p + o0 : nullptr;
+  for (int i = tid; i < Po * NQ; i += 256) {
+    const int px = i / NQ, q = i - px * NQ;
+    float4 v = *reinterpret_cast<const float4*>(red + px * NT + q * 4);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 t = *reinterpret_cast<const float4*>(red + ((size_t)w * MP + px) * NT + q * 4);
+      v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+    }
+    const float4 b = *reinterpret_cast<const float4*>(a.bp + o0 + q * 4);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    if (res) {
+      const float4 x = *reinterpret_cast<const float4*>(res + (size_t)px * a.cout_p + q * 4);
+      v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
+    }
+    *reinterpret_cast<float4*>(out + (size_t)px * a.cout_p + q * 4) = v;
+  }
+  stamp(a.stamps, 4);
+}
+
+// SE excitation for the wide blocks (features.9..11, C >= 288, whose fc2 is
+// too large to recompute in every project workgroup): one workgroup per
+// (image, 64 channels).  The image's fc1 partials and the 64-column slice of
+// W2 are loaded in one round trip; hid is summed in slice order, the slice's
+// excitation in j-group order (deterministic).  Writes sesc [N][Ep].
+__global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, float* __restrict__ sesc) {
+  __shared__ __attribute__((aligned(16))) float spart[kSeExcitePart];
+  __shared__ float hid[256];
+  __shared__ __attribute__((aligned(16))) float fsum[16 * 64];
+  const int n = blockIdx.y, c0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int npart = a.nsl * a.sq;
+  const float* part = a.part + (size_t)n * npart;
+  // work item: thread (q = channel quad of 16, grp = j group of 16)
+  const int q = tid & 15, grp = tid >> 4, jper = (a.sq + 15) / 16, j0 = grp * jper, j1 = min(a.sq, j0 + jper);
+  const bool qlive = c0 + q * 4 < a.C;
+  constexpr int JMAX = 9;   // sq <= 144
+  float4 wv[JMAX];
+#pragma unroll
+  for (int u = 0; u < JMAX; ++u)
+    if (qlive && j0 + u < j1) wv[u] = *reinterpret_cast<const float4*>(a.w2t + (size_t)(j0 + u) * a.C + c0 + q * 4);
+  {
+    constexpr int NP = kSeExcitePart / 4 / 256;
+    float4 v[NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u)   // clamped (unconditional) loads keep v in registers
+      v[u] = reinterpret_cast<const float4*>(part)[min(tid + u * 256, npart / 4 - 1)];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int i = tid + u * 256;
+      if (i < npart / 4) reinterpret_cast<float4*>(spart)[i] = v[u];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < a.sq; j += 256) {
+    float h = 0.f;
+    for (int s2 = 0; s2 < a.nsl; ++s2) h += spart[s2 * a.sq + j];
+    hid[j] = fmaxf(h + a.b1[j], 0.f);
+  }
+  __syncthreads();
+  float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < JMAX; ++u)
+    if (qlive && j0 + u < j1) {
+      const float h = hid[j0 + u];
+      acc4.x = fmaf(wv[u].x, h, acc4.x); acc4.y = fmaf(wv[u].y, h, acc4.y);
+      acc4.z = fmaf(wv[u].z, h, acc4.z); acc4.w = fmaf(wv[u].w, h, acc4.w);
+    }
+  reinterpret_cast<float4*>(fsum)[grp * 16 + q] = acc4;
+  __syncthreads();
+  if (tid < 64) {
+    const int c = c0 + tid;
+    float t = 0.f;
+#pragma unroll
+    for (int gi = 0; gi < 16; ++gi) t += fsum[gi * 64 + tid];
+    if (c < a.Ep) sesc[(size_t)n * a.Ep + c] = c < a.C ? kpd_hsigmoid(t + a.b2[c]) : 0.f;
   }
 }
 
@@ -839,22 +1139,76 @@ hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st) {
 
 size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
-  const size_t main = (a.we ? (size_t)a.cin_p * a.CS : 0) + (size_t)Pin * a.CS + (size_t)K * K * a.CS +
-                      (a.pooled ? (size_t)Po * a.CS : 0);
+  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)K * K * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) +
+                      (a.part ? (size_t)a.sq * a.CS : 0);
   return 4 * main;
 }
 
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
-  if (a.CS % 4 || a.Ep % a.CS || a.cin_p % 4) return hipErrorInvalidValue;
+  const int kc = a.cin_p / 16;
+  if ((a.CS != 16 && a.CS != 32) || a.Ep % a.CS || a.cin_p % 16 || (kc != 2 && kc != 3 && kc != 6) || !a.we ||
+      (a.part && (!a.pooled || !a.w1 || a.sq <= 0 || a.sq > 144 || a.C % 4)))
+    return hipErrorInvalidValue;
   const size_t lds = exdw_lds_bytes(a, K);
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(a.Ep / a.CS, N);
-#define EXDW(KK, SS) hipLaunchKernelGGL((exdw_kernel<KK, SS>), grid, dim3(256), lds, st, a)
+  const bool xt4 = a.Wo >= 12;
+#define EXDW_KC(KK, SS, NTC, XT)                                                                        \
+  do {                                                                                                  \
+    if (kc == 2) hipLaunchKernelGGL((exdw_kernel<KK, SS, NTC, XT, 2>), grid, dim3(256), lds, st, a);   \
+    else if (kc == 3) hipLaunchKernelGGL((exdw_kernel<KK, SS, NTC, XT, 3>), grid, dim3(256), lds, st, a); \
+    else hipLaunchKernelGGL((exdw_kernel<KK, SS, NTC, XT, 6>), grid, dim3(256), lds, st, a);           \
+  } while (0)
+#define EXDW(KK, SS)                                    \
+  do {                                                  \
+    if (a.CS == 16) {                                   \
+      if (xt4) EXDW_KC(KK, SS, 1, 4);                   \
+      else EXDW_KC(KK, SS, 1, 2);                       \
+    } else {                                            \
+      if (xt4) EXDW_KC(KK, SS, 2, 4);                   \
+      else EXDW_KC(KK, SS, 2, 2);                       \
+    }                                                   \
+  } while (0)
   if (K == 3 && S == 1) EXDW(3, 1);
-  else if (K == 3 && S == 2) EXDW(3, 2);
   else if (K == 5 && S == 1) EXDW(5, 1);
   else if (K == 5 && S == 2) EXDW(5, 2);
   else return hipErrorInvalidValue;
 #undef EXDW
+#undef EXDW_KC
   return hipGetLastError();
 }
+
+size_t seproj_lds_bytes(const SeProjArgs& a) {
+  const int mt = (a.Po + 15) / 16;
+  const size_t nq4 = a.C / 4, ngrp = std::max<size_t>(1, std::min<size_t>(16, 256 / nq4));
+  const size_t red = std::max({(size_t)4 * mt * 16 * a.NT, (size_t)a.nsl * a.sq, ngrp * a.C});
+  return 4 * ((size_t)a.Ep + 256 + red);
+}
+
+hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
+  const int mt = (a.Po + 15) / 16;
+  if (a.Ep % 16 || a.NT % 16 || a.cout_p % a.NT || a.sq > 144 || a.C > a.Ep || a.C % 4 ||
+      (size_t)a.nsl * a.sq > 6 * 256 * 4 || (a.nsl * a.sq) % 4)
+    return hipErrorInvalidValue;
+  const size_t lds = seproj_lds_bytes(a);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(a.cout_p / a.NT, N);
+  const int ntt = a.NT / 16;
+#define SEP(M, T) hipLaunchKernelGGL((seproj_kernel<M, T>), grid, dim3(256), lds, st, a)
+  if (mt == 3 && ntt == 1) SEP(3, 1);
+  else if (mt == 3 && ntt == 2) SEP(3, 2);
+  else if (mt == 3 && ntt == 3) SEP(3, 3);
+  else if (mt == 12 && ntt == 1) SEP(12, 1);
+  else if (mt == 12 && ntt == 3) SEP(12, 3);
+  else return hipErrorInvalidValue;
+#undef SEP
+  return hipGetLastError();
+}
+
+hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st) {
+  if (a.sq > 144 || a.C % 4 || a.C > a.Ep || (size_t)a.nsl * a.sq > kSeExcitePart || (a.nsl * a.sq) % 4)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(se_excite_kernel, dim3((a.Ep + 63) / 64, N), dim3(256), 0, st, a, sesc);
+  return hipGetLastError();
+}
+

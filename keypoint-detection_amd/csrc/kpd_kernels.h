@@ -110,7 +110,7 @@ hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st);
 struct ExDwArgs {
   const float* x;        // NHWC [N][Hi][Wi][cin_p]
   int Hi, Wi, cin_p;
-  const float* we;       // expand [Ep][cin_p] (BN folded); null: no expand (Ep == cin_p)
+  const float* we;       // expand [Ep][cin_p] (BN folded), cin_p a multiple of 16, <= 96
   const float* be;
   int act_e;
   const float* wd;       // depthwise [K*K][Ep] (BN folded), bias bd [Ep]
@@ -119,10 +119,33 @@ struct ExDwArgs {
   float* out;            // [N][Ho][Wo][Ep]
   int Ho, Wo;
   float* pooled;         // optional [N][Ep] channel means of out (SE squeeze)
-  int CS;                // expanded channels per workgroup (multiple of 4, divides Ep)
+  int CS;                // expanded channels per workgroup (16 or 32, divides Ep)
+  const float* w1;       // SE fc1 [sq][C] (row-major) for the partials
+  float* part;           // optional [N][Ep/CS][sq] fc1 partial products (needs pooled)
+  int sq, C;
+  unsigned long long* stamps;   // diagnostic phase stamps, [grid][8] (KPD_STAMPS), normally null
 };
 size_t exdw_lds_bytes(const ExDwArgs& a, int K);
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st);
+// SE excitation (from exdw_kernel's fc1 partials) + project 1x1 + residual
+// (body_kernels.hip, seproj_kernel)
+struct SeProjArgs {
+  const float* d;        // depthwise output [N][Po][Ep]
+  int Po, Ep;
+  const float* part;     // [N][nsl][sq] fc1 partials
+  int nsl, sq, C;
+  const float *b1, *w2t, *b2;   // fc1 bias [sq]; fc2 transposed [sq][C]; fc2 bias [C]
+  const float *wp, *bp;  // project [cout_p][Ep], [cout_p] (BN folded)
+  int cout_p, NT;        // output channels per workgroup (multiple of 16)
+  const float* res;      // optional residual [N][Po][cout_p]
+  float* out;            // [N][Po][cout_p]
+  unsigned long long* stamps;   // diagnostic phase stamps, [grid][8] (KPD_STAMPS), normally null
+  const float* sesc;     // optional precomputed excitation [N][Ep] (se_excite_kernel); null: computed here
+};
+size_t seproj_lds_bytes(const SeProjArgs& a);
+hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st);
+// the excitation alone, for the wide blocks: sesc [N][Ep]
+hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st);
 // sc_in != null: split output (f16 [hi32|lo32] groups, scale from split_a_exp)

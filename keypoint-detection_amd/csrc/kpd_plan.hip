@@ -119,6 +119,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
   float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
   float* pool = nullptr;    // [B][1024] SE channel means from the fused expand+depthwise kernel
+  float* separt = nullptr;  // [B][kSePartFloats] SE fc1 partials (exdw_kernel -> seproj_kernel)
   float* sc = nullptr;    // split FPN scale inputs: slotted max|tap0|, max|lateral1| (amax_publish)
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
@@ -198,6 +199,7 @@ struct kpd_plan {
   hipStream_t sub_st[kMaxSub] = {};       // [0] unused: sub-batch 0 runs on the caller's stream
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
   std::map<std::string, std::pair<const void*, size_t>> debug;
+  unsigned long long* stamps = nullptr;   // KPD_STAMPS diagnostic buffer (kStampWords)
   // per-stage HIP-event timing (kpd_plan_timing)
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; size_t used = 0; };
   bool timing = false;
@@ -486,7 +488,8 @@ int pack_fpn0x(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
 
 // ------------------------------------------------------------------ workspace
 constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
-constexpr int kFuseMaxPix = 16 * 12;        // input maps up to this size take the fused expand+depthwise
+constexpr int kFuseMaxPix = 32 * 24;        // input maps up to this size take the fused expand+depthwise
+constexpr int kSePartFloats = 8192;         // per image: (Ep / CS) slices x sq fc1 partials
 
 struct Carver {
   char* base;
@@ -521,6 +524,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.sc = c.take<float>(2 * kAmaxSlots * kAmaxStride);
   w.splitk = c.take<float>(kSplitKFloats);
   w.pool = c.take<float>((size_t)B * 1024);
+  w.separt = c.take<float>((size_t)B * kSePartFloats);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
@@ -692,6 +696,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   p->allocs.clear();
   p->fpn0s.hl = nullptr;
   p->fpn0x.w0 = p->fpn0x.weff = nullptr;
+  p->stamps = nullptr;
   p->pd = DevConv();
   p->anchors = nullptr;
   p->kh_ds1 = DevConv();
@@ -908,6 +913,23 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   g_splitk = w.splitk;
   std::map<std::string, std::pair<const void*, size_t>> dbg;
 
+  // KPD_STAMPS: per-workgroup phase stamps of the SE-block kernels (debug
+  // buffers "stamps_exdw_<i>" / "stamps_seproj_<i>", single-stream forwards)
+  static const bool want_stamps = getenv("KPD_STAMPS") != nullptr;
+  constexpr size_t kStampWords = 1 << 20;
+  if (want_stamps && !p->stamps) {
+    HIP_TRY(hipMalloc(&p->stamps, kStampWords * 8));
+    p->allocs.push_back(p->stamps);
+  }
+  size_t stamp_off = 0;
+  auto take_stamps = [&](const std::string& name, size_t wgs) -> unsigned long long* {
+    if (!want_stamps || !debug || stamp_off + wgs * 8 > kStampWords) return nullptr;
+    unsigned long long* r = p->stamps + stamp_off;
+    stamp_off += wgs * 8;
+    dbg[name] = {r, wgs * 64};
+    return r;
+  };
+
   // ---------------- MobileNetV3-Small body ----------------
   std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
   if (split) HIP_TRY(hipMemsetAsync(w.sc, 0, 2 * kAmaxSlots * kAmaxStride * sizeof(float), st));
@@ -951,15 +973,54 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
         continue;
       }
     }
-    if (!no_fuse && hi * wi <= kFuseMaxPix && (!bn.has_exp || bn.expand.cout_p == bn.dw.Cp)) {
-      for (int cs : {16, 32, 48}) {   // narrow slices: more workgroups for these small layers
-        xa.CS = cs;
-        if (bn.dw.Cp % cs == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 64 * 1024) { fused = true; break; }
-      }
+    if (!no_fuse && hi * wi <= kFuseMaxPix && bn.has_exp && bn.expand.cout_p == bn.dw.Cp && inp % 16 == 0 &&
+        inp <= 96) {
+      // slice width fixed per layer (never per batch: the fc1 partial sums
+      // must not depend on what an image is batched with)
+      static const int cs_env = getenv("KPD_EXDW_CS") ? atoi(getenv("KPD_EXDW_CS")) : 0;   // A/B sweeps
+      xa.CS = cs_env > 0 ? cs_env : (bn.dw.Cp >= 288 ? 32 : 16);
+      fused = bn.dw.Cp % xa.CS == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 160 * 1024;
     }
+    // SE blocks on the coarse maps: fc1 partials in exdw_kernel, then the
+    // excitation + project (+ residual) in one seproj_kernel launch
+    static const bool no_seproj = getenv("KPD_NO_SEPROJ") != nullptr;   // A/B switch
+    const bool seproj = fused && bn.cfg.se && !no_seproj && bn.project.k == 1 && !bn.project.bf16 &&
+                        bn.project.cin_p == bn.dw.Cp && bn.se.sq <= 144 && bn.se.C % 4 == 0 &&
+                        (ho * wo == 48 || ho * wo == 192) && (size_t)(bn.dw.Cp / xa.CS) * bn.se.sq <= kSePartFloats;
     if (fused) {
+      if (seproj) {
+        xa.part = w.separt; xa.w1 = bn.se.w1; xa.sq = bn.se.sq; xa.C = bn.se.C;
+      }
+      xa.stamps = take_stamps("stamps_exdw_" + std::to_string(i), (size_t)(bn.dw.Cp / xa.CS) * B);
       HIP_TRY(launch_exdw(xa, B, bn.dw.k, bn.dw.s, st));
-    } else {
+    }
+    if (seproj) {
+      SeProjArgs sa{};
+      sa.d = w.d[i]; sa.Po = ho * wo; sa.Ep = bn.dw.Cp;
+      sa.part = w.separt; sa.nsl = bn.dw.Cp / xa.CS; sa.sq = bn.se.sq; sa.C = bn.se.C;
+      sa.b1 = bn.se.b1; sa.w2t = bn.se.w2; sa.b2 = bn.se.b2;
+      sa.wp = static_cast<const float*>(bn.project.w); sa.bp = bn.project.b; sa.cout_p = bn.project.cout_p;
+      static const int nt_env = getenv("KPD_SEPROJ_NT") ? atoi(getenv("KPD_SEPROJ_NT")) : 0;
+      sa.NT = nt_env > 0 ? nt_env : (sa.Po == 48 ? 32 : 16);
+      if (sa.cout_p % sa.NT) sa.NT = 16;
+      const bool res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
+      sa.res = res ? x : nullptr;
+      sa.out = w.o[i];
+      // wide blocks (C >= 288): the excitation as its own launch (one fc2
+      // pass per image instead of one per project workgroup)
+      static const int se_split_env = getenv("KPD_SE_SPLIT") ? atoi(getenv("KPD_SE_SPLIT")) : -1;   // A/B
+      if (se_split_env == 1 || (se_split_env < 0 && bn.se.C >= 288)) {
+        HIP_TRY(launch_se_excite(sa, B, w.sesc[i], st));
+        sa.sesc = w.sesc[i];
+      }
+      sa.stamps = take_stamps("stamps_seproj_" + std::to_string(i), (size_t)(sa.cout_p / sa.NT) * B);
+      HIP_TRY(launch_seproj(sa, B, st));
+      x = w.o[i];
+      if (i + 1 == 3) taps[1] = x;
+      if (i + 1 == 8) taps[2] = x;
+      continue;
+    }
+    if (!fused) {
       const float* e = x;
       if (bn.has_exp) {
         if (int rc = conv(bn.expand, x, B, hi, wi, inp, w.e[i], bn.cfg.act, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
