@@ -169,6 +169,19 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
   }
   const int kc_per_tap = cin_e / 64;
   const int KT = (DBG & 16) ? 0 : KS * KS * kc_per_tap;
+  // fused final layer: its [17][64] weights + [17] bias, loaded now (3 per
+  // thread) so the epilogue does not wait on a global round trip
+  float fin_pre[3] = {0.f, 0.f, 0.f};
+  if constexpr (BN == 64 && std::is_same<TO, float>::value) {
+    if (p.fin_w) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = tid + u * NT;
+        if (i < 17 * 64) fin_pre[u] = p.fin_w[i];
+        else if (i < 17 * 65) fin_pre[u] = p.fin_b[i - 17 * 64];
+      }
+    }
+  }
 
   // loader state (wave-uniform): next K-tile to issue as (tap, kc)
   int ld_tap = 0, ld_kc = 0;
@@ -395,6 +408,77 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
       float* st = p.stats + ((size_t)n * p.tiles_per_img + t) * 2 * p.cout_p;
       st[n0 + tid] = sm;
       st[p.cout_p + n0 + tid] = mx;
+    }
+  }
+  // (3') HeatmapHead final_layer fused (heatmap_head.py:41-45; mixed mode,
+  // BN = 64 = all conv-3 channels of a pixel in the tile): per pixel 17 dot
+  // products of length 64 + sigmoid, written straight into the reference's
+  // [B][P][17][56][56] heatmap at the box's slot (zeros for a padding slot).
+  // After the quad transpose a lane holds channels j*16 + 4*q4 .. +3 of one
+  // pixel; the 4 lanes of a pixel (q4 = lane bits 2-3) combine by two xor
+  // shuffles.  conv 3's own output is never written.
+  if constexpr (BN == 64 && std::is_same<TO, float>::value) {
+    if (p.fin_w) {
+      constexpr int NKF = 17;
+      float* fw = reinterpret_cast<float*>(lds);   // [17][64] + [17]: the ring is free after the K loop
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = tid + u * NT;
+        if (i < NKF * 65) fw[i] = fin_pre[u];
+      }
+      __syncthreads();
+      f32x4 v[FM][FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          v[i][j] = acc[i][j];
+          quad_transpose(v[i][j], t4);
+        }
+      float o[FM][NKF];
+#pragma unroll
+      for (int k = 0; k < NKF; ++k) {
+        float a[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const float4 w4 = *reinterpret_cast<const float4*>(fw + k * 64 + j * 16 + q4 * 4);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            a[i] = fmaf(w4.x, v[i][j][0], a[i]); a[i] = fmaf(w4.y, v[i][j][1], a[i]);
+            a[i] = fmaf(w4.z, v[i][j][2], a[i]); a[i] = fmaf(w4.w, v[i][j][3], a[i]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          a[i] += __shfl_xor(a[i], 4);
+          a[i] += __shfl_xor(a[i], 8);
+          o[i][k] = a[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = m0 + wm * WM + i * 16 + g * 4 + t4;
+        if (row < M) {
+          const int rl = row / HW, pix = row - rl * HW, r = p.r0 + rl;   // r0: the launch chunk's first ROI
+          const int sl = p.slot[r], bimg = r / p.P;
+          const int pos = sl >= 0 ? sl : slot_pos(sl);
+          float* dst = p.heat + ((size_t)(bimg * p.P + pos) * NKF) * HW + pix;
+          // lane q4 stores k = q4, q4 + 4, ... (every store instruction has all lanes active)
+#pragma unroll
+          for (int s4 = 0; s4 < (NKF + 3) / 4; ++s4) {
+            const int k = s4 * 4 + q4;
+            float val = q4 == 0 ? o[i][s4 * 4] : 0.f;
+            if (s4 * 4 + 1 < NKF && q4 == 1) val = o[i][s4 * 4 + 1];
+            if (s4 * 4 + 2 < NKF && q4 == 2) val = o[i][s4 * 4 + 2];
+            if (s4 * 4 + 3 < NKF && q4 == 3) val = o[i][s4 * 4 + 3];
+            if (k < NKF) dst[(size_t)k * HW] = sl >= 0 ? kpd_sigmoid(val + fw[NKF * 64 + k]) : 0.f;
+          }
+        }
+      }
+      return;
     }
   }
   // (3) transposed 16-byte row stores
@@ -709,6 +793,7 @@ hipError_t launch(const Conv16Args& a0, hipStream_t st) {
     a.out = static_cast<char*>(a0.out) + n0 * HW * a.out_cstride * OS;
     a.stats = a0.stats ? a0.stats + (long)n0 * a.tiles_per_img * 2 * a.cout_p : nullptr;
     a.in_bytes = (int)(nb * img_bytes);
+    a.r0 = a0.r0 + n0;
     dim3 grid(((a.M + BM - 1) / BM) * (a.cout_p / BN));
     hipLaunchKernelGGL((conv16_kernel<SPLIT, TO, KS, BN, S, PF>), grid, dim3(NT), 0, st, a);
     const hipError_t e = hipGetLastError();

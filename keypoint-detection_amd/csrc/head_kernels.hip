@@ -121,33 +121,62 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
 #pragma unroll
   for (int q = 0; q < CW; ++q) ch[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
 
-  float s_sum = 0.f, s_max = -INFINITY;
-  for (int pw = wave; pw < HM; pw += 4) {
-    float acc[CW];
+  // The wave's 14 bins (pw = wave + 4 j) advance together through the
+  // sampling grid: for each (iy, ix) the 4 corner loads of all 14 bins are
+  // issued before any is used (56 gathers in flight per lane instead of one
+  // bin's 4), and every bin still sums its samples in (iy, ix) order, i.e. the
+  // arithmetic is the scalar loop's.  A sample outside [-1, H] x [-1, W]
+  // contributes 0 (torchvision's skip).
+  constexpr int NB = HM / 4;
+  float acc[NB][CW];
 #pragma unroll
-    for (int q = 0; q < CW; ++q) acc[q] = 0.f;
-    for (int iy = 0; iy < gh; ++iy) {
-      float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
-      for (int ix = 0; ix < gw; ++ix) {
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int q = 0; q < CW; ++q) acc[j][q] = 0.f;
+  for (int iy = 0; iy < gh; ++iy) {
+    float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
+    const bool yin = !(y < -1.f || y > (float)Hf);
+    float yy = y <= 0.f ? 0.f : y;
+    int yl = (int)yy, yh;
+    if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
+    const float ly = yy - (float)yl, hy = 1.f - ly;
+    for (int ix = 0; ix < gw; ++ix) {
+      float v[NB][4][CW], wgt[NB][4];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int pw = wave + 4 * j;
         float x = x1 + (float)pw * bin_w + ((float)ix + 0.5f) * bin_w / (float)gw;
-        if (y < -1.f || y > (float)Hf || x < -1.f || x > (float)Wf) continue;
-        float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
-        int yl = (int)yy, xl = (int)xx, yh, xh;
-        if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
+        const bool in = yin && !(x < -1.f || x > (float)Wf);
+        float xx = x <= 0.f ? 0.f : x;
+        int xl = (int)xx, xh;
         if (xl >= Wf - 1) { xh = xl = Wf - 1; xx = (float)xl; } else xh = xl + 1;
-        const float ly = yy - (float)yl, lx = xx - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
+        const float lx = xx - (float)xl, hx = 1.f - lx;
+        wgt[j][0] = in ? hy * hx : 0.f; wgt[j][1] = in ? hy * lx : 0.f;
+        wgt[j][2] = in ? ly * hx : 0.f; wgt[j][3] = in ? ly * lx : 0.f;
         const float* p1 = fb + ((size_t)yl * Wf + xl) * Cf;
         const float* p2 = fb + ((size_t)yl * Wf + xh) * Cf;
         const float* p3 = fb + ((size_t)yh * Wf + xl) * Cf;
         const float* p4 = fb + ((size_t)yh * Wf + xh) * Cf;
 #pragma unroll
-        for (int q = 0; q < CW; ++q)
-          acc[q] += hy * hx * p1[ch[q]] + hy * lx * p2[ch[q]] + ly * hx * p3[ch[q]] + ly * lx * p4[ch[q]];
+        for (int q = 0; q < CW; ++q) {
+          v[j][0][q] = p1[ch[q]]; v[j][1][q] = p2[ch[q]]; v[j][2][q] = p3[ch[q]]; v[j][3][q] = p4[ch[q]];
+        }
       }
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < CW; ++q)
+          acc[j][q] += wgt[j][0] * v[j][0][q] + wgt[j][1] * v[j][1][q] + wgt[j][2] * v[j][2][q] +
+                       wgt[j][3] * v[j][3][q];
     }
+  }
+  float s_sum = 0.f, s_max = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int pw = wave + 4 * j;
 #pragma unroll
     for (int q = 0; q < CW; ++q) {
-      const float v = acc[q] / count;
+      const float v = acc[j][q] / count;
       roi[(((size_t)r * HM + ph) * HM + pw) * CO + lane + TOPK * q] = v;
       s_sum += v;
       s_max = fmaxf(s_max, v);

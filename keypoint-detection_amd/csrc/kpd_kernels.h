@@ -46,6 +46,14 @@ struct Conv16Args {
   float sc_maxb, sc_maxs;
   int w_exp;
   int in_bytes, wt_bytes;   // filled by the launcher
+  // optional fused HeatmapHead final_layer (1x1 64->17 + sigmoid) for the
+  // BN = 64 fp32-out conv: heatmap [B][P][17][H][W] at the ROI's slot
+  const float* fin_w;    // [17][64]
+  const float* fin_b;    // [17]
+  const int32_t* slot;   // [R] (launch_slotmap)
+  int P;
+  float* heat;
+  int r0;                // first ROI of this launch (set by the launcher per chunk)
 };
 hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st);
 

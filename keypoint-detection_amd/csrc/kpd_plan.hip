@@ -627,9 +627,17 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
 // HeatmapHead 3x3 conv + bias + BN + ReLU on the 56x56 ROI maps: bf16 weights
 // go to the LDS-DMA kernel (conv_glds.hip), fp32 to the generic one.
 // out_kind: 1 = bf16 output, 2 = fp32 output (bf16 weights); fp32 otherwise.
-int hm_conv(const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind, hipStream_t st) {
+// fin (bf16 path, out_kind 2 only): fuse the final 1x1 + sigmoid into the
+// epilogue and write the heatmap instead of `out` (conv_glds.hip).
+struct HmFinal { const float *w, *b; const int32_t* slot; int P; float* heat; };
+int hm_conv(const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind, hipStream_t st,
+            const HmFinal* fin = nullptr) {
   if (!L.bf16) return conv(L, in, R, 56, 56, in_cstride, out, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
   Conv16Args a{};
+  if (fin) {
+    if (out_kind != 2 || L.cout_p != 64) return fail(KPD_EINVAL, "fused final layer needs the 64-channel conv");
+    a.fin_w = fin->w; a.fin_b = fin->b; a.slot = fin->slot; a.P = fin->P; a.heat = fin->heat;
+  }
   a.in = in; a.wt = L.w; a.bias = L.b; a.out = out;
   a.N = R; a.H = 56; a.W = 56; a.cin_e = L.cin_p; a.cout_p = L.cout_p; a.in_cstride = in_cstride;
   a.out_cstride = L.cout_p; a.act = ACT_RELU; a.M = R * 56 * 56;
@@ -1156,11 +1164,15 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   if (int rc = hm_conv(p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st)) return rc;
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
-  if (int rc = hm_conv(p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st)) return rc;
+  // mixed: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
+  static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
+  const bool fin_fused = p->hm3.bf16 && p->hm3.cout_p == 64 && !no_fin_fuse;
+  const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
+  if (int rc = hm_conv(p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr)) return rc;
   c3.reset();
   {
     Stage sg(p, "hm_final_decode", st);
-    HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
+    if (!fin_fused) HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
     HIP_TRY(launch_decode(heat_out, boxes, w.slot, R, P, kpts, vis, st));
   }
   if (dual) {
