@@ -312,6 +312,61 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
       step(kt + 1, f1, f0);
     }
     if (kt < KT) step(kt, f0, f1);
+  } else if constexpr (!SPLIT && (DBG & 0x10000) == 0) {
+    // Half-tile phases (bf16): the two 32-deep k-steps q = 0 / 1 of a K-tile
+    // use separate fragment registers, so the reads of one overlap the MFMAs
+    // of the other and the pipe never waits on LDS latency behind a barrier:
+    //   reads (kt, q1) | MFMAs (kt, q0) | barrier kt+1 | reads (kt+1, q0) | MFMAs (kt, q1)
+    // Same registers as one whole-tile fragment set.  The stage of tile kt is
+    // free at barrier kt+1 (every wave's reads of it retired by the lgkmcnt(0)
+    // in front of that barrier), which is where tile kt+S is issued into it.
+    struct Half { uint4 a[FM], b[FN]; };
+    auto load_half = [&](int stage, int q, Half& f) {
+      const char* sb = lds + stage * STAGE;
+      const int chq = q ? ch1 : ch0;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) f.b[j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + chq);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) f.a[i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + chq);
+    };
+    auto mma_half = [&](const Half& f) {
+      if constexpr ((DBG & 2) != 0) {
+        acc[0][0][0] += __uint_as_float(f.a[0].x ^ f.b[FN - 1].w);
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
+                                                              __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
+    };
+    Half f0, f1;
+    int cs = 0, is = S - 1;
+    if (KT > 0) {
+      tile_ready(0);
+      if (S - 1 < KT) issue(is);   // tile S-1 into the never-used stage S-1
+      is = is + 1 == S ? 0 : is + 1;
+      load_half(0, 0, f0);
+    }
+    for (int kt = 0; kt < KT; ++kt) {
+      load_half(cs, 1, f1);
+      __builtin_amdgcn_s_setprio(1);
+      mma_half(f0);
+      __builtin_amdgcn_s_setprio(0);
+      cs = cs + 1 == S ? 0 : cs + 1;
+      if (kt + 1 < KT) {
+        tile_ready(kt + 1);   // f1 complete, tile kt+1 visible, stage of tile kt free
+        if (kt + S < KT) issue(is);
+        is = is + 1 == S ? 0 : is + 1;
+        load_half(cs, 0, f0);
+      } else {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+      __builtin_amdgcn_s_setprio(1);
+      mma_half(f1);
+      __builtin_amdgcn_s_setprio(0);
+    }
   } else {
     int cs = 0, is = S - 1;
     for (int kt = 0; kt < KT; ++kt) {
@@ -773,6 +828,255 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
   *reinterpret_cast<f16x8v*>(o + G) = lo;
 }
 
+// ---------------------------------------------------------------- HeatmapHead convs, padded ROI maps
+// 3x3 conv + folded BN + ReLU on the 56x56 ROI maps of HeatmapHead
+// (heatmap_head.py:31-45,55-66), bf16 operands, fp32 accumulation.  The
+// activations are stored with a one-pixel zero border, [R][58][58][C], so a
+// tap (dy, dx) of output position m is input position m + 58 dy + dx with the
+// zero padding already in memory.  A GEMM row is a padded position; a tile is
+// 256 consecutive positions, and its A operand for ALL nine taps of a
+// 64-channel chunk is one window of 384 positions (m0 - 64 .. m0 + 319) staged
+// once per chunk -- the per-tap A staging of the generic kernel (9 x 256 rows)
+// becomes 384 rows, so the LDS-DMA bytes per MFMA drop 1.7x (BN 256) to 3x
+// (BN 64): the generic kernel is bound by the ~70 GB/s per CU an L2 -> LDS
+// DMA stream sustains (tools/conv16_probe.py ablations).  The border rows and
+// columns of the GEMM are computed and discarded (the tile range starts at
+// padded row 1 of ROI 0; ~7 % extra MFMA work); outputs are stored to the
+// interior only, so the zero border written once at workspace creation stays.
+//   BN 256: bf16 output (conv 1, 2), LDS-staged epilogue.
+//   BN 64 : conv 3 with the final 1x1 64->17 + sigmoid fused (mixed mode),
+//           written to the [B][P][17][56][56] heatmap at the ROI's slot.
+constexpr int HP = 58, HPP = HP * HP;   // padded ROI side, positions per ROI
+constexpr int AWIN = 384;               // A window rows per chunk
+template <int BN, int SB>
+__global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
+  constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
+  constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
+  constexpr int A_LD = AWIN / 8 / 8;                     // A-window DMA wave-instructions per wave (6)
+  constexpr int B_LD = BN / 64;                          // B DMA wave-instructions per wave per K-step
+  constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB;
+  constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
+  constexpr bool FINAL = BN == 64;
+  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BM, 128, NT>();
+  constexpr int LDS = RING > EPI ? RING : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int NTL = p.cout / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = HP + (L / NTL) * BM, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
+  const int Mtot = p.R * HPP, cin = p.cin, NC = cin / 64, KT = 9 * NC;
+  const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
+  const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
+  const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
+  // A window: wave w fills rows [48 w, 48 w + 48) of the window
+  unsigned a_off[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int m = m0 - 64 + wave * (AWIN / 8) + i * 8 + lrow;
+    a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)(m * cin * 2 + lchunk * 16) : OOB;
+  }
+  unsigned b_off[B_LD];
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int co = n0 + wave * (BN / 8) + i * 8 + lrow;
+    b_off[i] = (unsigned)((co * 9 * cin) * 2 + lchunk * 16);
+  }
+  auto issue_a = [&](int c, int i) {   // A window of chunk c, wave-instruction i
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / 8) + i * 8) * ROWB);
+    glds16(rin, dst, a_off[i] == OOB ? OOB : a_off[i] + c * 128, 0);
+  };
+  auto issue_b = [&](int k) {          // B K-step k = (chunk, tap) into stage k % SB
+    const int c = k / 9, t = k - c * 9;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + wave * (BN / 8) * ROWB);
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], (t * cin + c * 64) * 2);
+  };
+  // Barrier of K-step k: B(k) landed.  A-window pieces are issued before the
+  // B of the same batch, so every DMA younger than B(k) is among the
+  // (SB - 2) * B_LD weight loads of later steps or an A piece issued after
+  // them: vmcnt((SB - 2) * B_LD) retires B(k) -- and the window of k's chunk,
+  // whose last piece (tap 5 of the previous chunk) precedes B(k) whenever
+  // SB <= 4.  Then every fragment read retired, all waves here.
+  static_assert(SB >= 2 && SB <= 4, "weight ring");
+  auto barrier_k = [&](bool tail) {
+    if (tail) wait_vmcnt<0>();
+    else wait_vmcnt<(SB - 2) * B_LD>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, r16 = lane & 15;
+  const int b_row = (wn * 64 + r16) * ROWB;
+  const int bch0 = ((g ^ (r16 & 7)) << 4), bch1 = (((4 + g) ^ (r16 & 7)) << 4);
+  struct Half { uint4 a[FM], b[FN]; };
+  // half q of K-step k: A rows shifted by the tap offset (swizzle by the row)
+  auto load_half = [&](int k, int q, Half& f) {
+    const int c = k / 9, t = k - c * 9, off = (t / 3 - 1) * HP + (t % 3 - 1);
+    const char* ab = lds + (c & 1) * ABUF;
+    const char* bb = lds + 2 * ABUF + (k % SB) * BSTAGE;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) f.b[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
+    const int r0w = wm * WM + r16 + 64 + off;   // window row of fragment 0 (rows of fragment i: + 16 i)
+    const int ach = (((q ? 4 : 0) + g) ^ (r0w & 7)) << 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) f.a[i] = *reinterpret_cast<const uint4*>(ab + (r0w + i * 16) * ROWB + ach);
+  };
+  auto mma_half = [&](const Half& f) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
+                                                            __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
+  };
+  // fused final layer weights, loaded before the K loop (3 per thread)
+  float fin_pre[3] = {0.f, 0.f, 0.f};
+  if constexpr (FINAL) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int i = tid + u * NT;
+      if (i < 17 * 64) fin_pre[u] = p.fin_w[i];
+      else if (i < 17 * 65) fin_pre[u] = p.fin_b[i - 17 * 64];
+    }
+  }
+  // prologue: chunk 0's window and the first SB-1 K-steps' weights
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) issue_a(0, i);
+#pragma unroll
+  for (int k = 0; k < SB - 1; ++k)
+    if (k < KT) issue_b(k);
+  Half f0, f1;
+  barrier_k(KT < SB - 1);
+  if (NC > 1) issue_a(1, 0);
+  if (SB - 1 < KT) issue_b(SB - 1);
+  load_half(0, 0, f0);
+  // K-step k: reads (k, q1) | MFMAs (k, q0) | barrier k+1 + DMA issue | reads (k+1, q0) | MFMAs (k, q1)
+  for (int k = 0; k < KT; ++k) {
+    load_half(k, 1, f1);
+    __builtin_amdgcn_s_setprio(1);
+    mma_half(f0);
+    __builtin_amdgcn_s_setprio(0);
+    if (k + 1 < KT) {
+      const int k1 = k + 1, c1 = k1 / 9, t1 = k1 - c1 * 9;
+      barrier_k(k1 + SB - 2 >= KT);   // B(k1) and its chunk's window landed; reads of k retired
+      if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);   // next chunk's window, spread over taps
+      if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);         // into the stage of B(k)
+      load_half(k1, 0, f0);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    mma_half(f1);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();
+
+  // interior test of a padded position: ROI row/column 1..56
+  auto interior = [&](int m, int& r, int& yy, int& xx) {
+    r = m / HPP;
+    const int rem = m - r * HPP;
+    yy = rem / HP - 1;
+    xx = rem - (yy + 1) * HP - 1;
+    return m < Mtot - HP && yy >= 0 && yy < HP - 2 && xx >= 0 && xx < HP - 2;
+  };
+  if constexpr (!FINAL) {
+    // bias + ReLU, bf16, 16-byte row stores through the LDS tile (two 128-column halves)
+    float* tile = reinterpret_cast<float*>(lds);
+    constexpr int P4 = 128 + 4, C4 = 32, RS = NT / C4, IT = BM / RS;
+    __bf16* out = reinterpret_cast<__bf16*>(p.out);
+#pragma unroll
+    for (int h = 0; h < BN / 128; ++h) {
+      if (h) __syncthreads();
+      if (wn / 2 == h) acc_to_lds<FM, FN, WM, 64, 128>(tile, acc, wm, wn % 2, lane);
+      __syncthreads();
+      const int c4 = tid % C4, row0 = tid / C4, co = n0 + h * 128 + c4 * 4;
+      const float4 b = *reinterpret_cast<const float4*>(p.bias + co);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int row = row0 + it * RS, m = m0 + row;
+        int r, yy, xx;
+        if (!interior(m, r, yy, xx)) continue;
+        float4 x = *reinterpret_cast<const float4*>(tile + row * P4 + c4 * 4);
+        x.x = fmaxf(x.x + b.x, 0.f); x.y = fmaxf(x.y + b.y, 0.f);
+        x.z = fmaxf(x.z + b.z, 0.f); x.w = fmaxf(x.w + b.w, 0.f);
+        store4<__bf16>(out + (size_t)m * p.cout + co, x);
+      }
+    }
+  } else {
+    // conv 3 (64 channels, bias + ReLU) -> final 1x1 64->17 + sigmoid per pixel
+    constexpr int NKF = 17;
+    float* fw = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int i = tid + u * NT;
+      if (i < NKF * 65) fw[i] = fin_pre[u];
+    }
+    __syncthreads();
+    const int t4 = lane & 3, q4 = r16 >> 2;
+    f32x4 v[FM][FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const float bj = p.bias[j * 16 + r16];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e] + bj, 0.f);
+        v[i][j] = acc[i][j];
+        quad_transpose(v[i][j], t4);
+      }
+    }
+    float o[FM][NKF];
+#pragma unroll
+    for (int k = 0; k < NKF; ++k) {
+      float a[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float4 w4 = *reinterpret_cast<const float4*>(fw + k * 64 + j * 16 + q4 * 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          a[i] = fmaf(w4.x, v[i][j][0], a[i]); a[i] = fmaf(w4.y, v[i][j][1], a[i]);
+          a[i] = fmaf(w4.z, v[i][j][2], a[i]); a[i] = fmaf(w4.w, v[i][j][3], a[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        a[i] += __shfl_xor(a[i], 4);
+        a[i] += __shfl_xor(a[i], 8);
+        o[i][k] = a[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + g * 4 + t4;
+      int rl, yy, xx;
+      if (!interior(m, rl, yy, xx)) continue;
+      const int r = p.r0 + rl, sl = p.slot[r], bimg = r / p.P;
+      const int pos = sl >= 0 ? sl : slot_pos(sl);
+      float* dst = p.heat + ((size_t)(bimg * p.P + pos) * NKF) * ((HP - 2) * (HP - 2)) + yy * (HP - 2) + xx;
+#pragma unroll
+      for (int s4 = 0; s4 < (NKF + 3) / 4; ++s4) {
+        const int k = s4 * 4 + q4;
+        float val = q4 == 0 ? o[i][s4 * 4] : 0.f;
+        if (s4 * 4 + 1 < NKF && q4 == 1) val = o[i][s4 * 4 + 1];
+        if (s4 * 4 + 2 < NKF && q4 == 2) val = o[i][s4 * 4 + 2];
+        if (s4 * 4 + 3 < NKF && q4 == 3) val = o[i][s4 * 4 + 3];
+        if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? kpd_sigmoid(val + fw[NKF * 64 + k]) : 0.f;
+      }
+    }
+  }
+}
+
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
 
 template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF = (BN <= 128)>
@@ -821,6 +1125,39 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
   if (a.cout_p % 64 == 0)
     return out_bf16 ? launch<false, __bf16, 3, 64, 3>(a, st) : launch<false, float, 3, 64, 3>(a, st);
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
+  if (a0.R <= 0) return hipSuccess;
+  const bool fin = a0.fin_w != nullptr;
+  if (a0.cin % 64 || (fin ? a0.cout != 64 : a0.cout % 128) || (fin && (!a0.slot || !a0.heat || !a0.fin_b)) ||
+      (!fin && !a0.out))
+    return hipErrorInvalidValue;
+  HmConvArgs a = a0;
+  const long wt_bytes = (long)a.cout * 9 * a.cin * 2, roi_bytes = (long)HPP * a.cin * 2;
+  if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
+  a.wt_bytes = (int)wt_bytes;
+  const int chunk = (int)std::min<long>(a0.R, kMaxDesc / roi_bytes);
+  for (int r0 = 0; r0 < a0.R; r0 += chunk) {
+    const int nr = std::min(chunk, a0.R - r0);
+    a.R = nr;
+    a.r0 = a0.r0 + r0;
+    a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
+    if (!fin) a.out = static_cast<__bf16*>(a0.out) + (size_t)r0 * HPP * a.cout;
+    a.in_bytes = (int)(nr * roi_bytes);
+    const long rows = (long)nr * HPP - 2 * HP;
+    // BN 256 with a 2-stage weight ring measured faster than BN 128 with 4
+    // stages for conv 1 / 2 (89 / 233 us vs 92 / 256 us at 64 ROIs): the
+    // wider tile halves the weight bytes per MFMA; conv 3 has 64 outputs
+    const int bn = fin ? 64 : (a.cout % 256 == 0 ? 256 : 128);
+    const dim3 grid((unsigned)(((rows + BM - 1) / BM) * (a.cout / bn)));
+    if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
+    else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((hmconv_kernel<128, 4>), grid, dim3(NT), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {

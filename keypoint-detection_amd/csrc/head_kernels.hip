@@ -283,7 +283,9 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
   const size_t pix = ((size_t)r * HM + y) * HM + x;
   const float4* src = reinterpret_cast<const float4*>(roi + pix * TOPK);
   if (out_bf16) {
-    __bf16* dst = reinterpret_cast<__bf16*>(xs) + pix * TOPK;
+    // out_bf16 == 2: the zero-bordered [R][58][58][64] layout of hmconv_kernel
+    const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + x + 1 : pix;
+    __bf16* dst = reinterpret_cast<__bf16*>(xs) + opix * TOPK;
 #pragma unroll
     for (int q = 0; q < TOPK / 8; ++q) {
       const float4 u = src[2 * q], v = src[2 * q + 1];

@@ -57,6 +57,26 @@ struct Conv16Args {
 };
 hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st);
 
+// HeatmapHead 3x3 conv on zero-bordered ROI maps [R][58][58][C] bf16
+// (conv_glds.hip, hmconv_kernel).  fin_w == null: bf16 output in the same
+// padded layout (interior only); else cout == 64 and the final 1x1 + sigmoid
+// is fused, writing heat [B][P][17][56][56] at the ROI's slot.
+struct HmConvArgs {
+  const void* in;        // [R][58][58][cin] bf16
+  const void* wt;        // [cout][9][cin] bf16 (BN folded)
+  const float* bias;     // [cout]
+  void* out;             // [R][58][58][cout] bf16
+  int R, cin, cout;
+  const float *fin_w, *fin_b;   // [17][64], [17]
+  const int32_t* slot;
+  int P;
+  float* heat;
+  int r0;                // first ROI of the launch chunk (launcher)
+  int in_bytes, wt_bytes;   // launcher
+};
+hipError_t launch_hmconv(const HmConvArgs& a, hipStream_t st);
+constexpr int kHmPad = 58;   // padded ROI side of the hmconv layout
+
 // FPN level 0 by linearity (split mode): conv3x3(L0(tap0) + up4(lat1)) =
 // conv3x3'(tap0) [composite weights W3.L0, 16 input channels]
 // + per-position-class combinations of lat1 [taps summed by the lat1 pixel they

@@ -503,6 +503,13 @@ struct Carver {
   }
 };
 
+// mixed precision runs the HeatmapHead convs on zero-bordered ROI maps
+// (hmconv_kernel); KPD_NO_HMCONV=1 keeps the unpadded generic conv (A/B)
+bool hm_padded(const kpd_plan* p) {
+  static const bool off = getenv("KPD_NO_HMCONV") != nullptr;
+  return p->precision == KPD_PRECISION_MIXED && !off;
+}
+
 size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   Carver c{base};
   const int B = d.B;
@@ -535,9 +542,11 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
     w.roi_stats = c.take<float>(R * 56 * 2 * 64);
     w.cw = c.take<float>(R * 64);
     w.smap = c.take<float>(px * 2);
-    w.xs = c.take<char>(px * 64 * es);
-    w.h1 = c.take<char>(px * 256 * es);
-    w.h2 = c.take<char>(px * 256 * es);
+    // mixed: zero-bordered 58x58 ROI maps for the padded heatmap convs (hmconv_kernel)
+    const size_t pxp = hm_padded(p) ? R * kHmPad * kHmPad : px;
+    w.xs = c.take<char>(pxp * 64 * es);
+    w.h1 = c.take<char>(pxp * 256 * es);
+    w.h2 = c.take<char>(pxp * 256 * es);
     w.h3 = c.take<float>(px * 64);
     w.heat = c.take<float>(R * 17 * 3136);
     if (d.flags & KPD_FLAG_DUAL_HEAD) {
@@ -630,9 +639,22 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
 // fin (bf16 path, out_kind 2 only): fuse the final 1x1 + sigmoid into the
 // epilogue and write the heatmap instead of `out` (conv_glds.hip).
 struct HmFinal { const float *w, *b; const int32_t* slot; int P; float* heat; };
-int hm_conv(const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind, hipStream_t st,
-            const HmFinal* fin = nullptr) {
+int hm_conv(const kpd_plan* p, const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind,
+            hipStream_t st, const HmFinal* fin = nullptr) {
   if (!L.bf16) return conv(L, in, R, 56, 56, in_cstride, out, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
+  if (hm_padded(p)) {
+    if (in_cstride != L.cin_p) return fail(KPD_EINVAL, "hmconv: input channel stride must equal cin");
+    HmConvArgs h{};
+    h.in = in; h.wt = L.w; h.bias = L.b; h.out = out; h.R = R; h.cin = L.cin_p; h.cout = L.cout_p;
+    if (fin) {
+      if (out_kind != 2 || L.cout_p != 64) return fail(KPD_EINVAL, "fused final layer needs the 64-channel conv");
+      h.fin_w = fin->w; h.fin_b = fin->b; h.slot = fin->slot; h.P = fin->P; h.heat = fin->heat;
+    } else if (out_kind != 1) {
+      return fail(KPD_EINVAL, "hmconv: bf16 output or the fused final layer only");
+    }
+    HIP_TRY(launch_hmconv(h, st));
+    return KPD_OK;
+  }
   Conv16Args a{};
   if (fin) {
     if (out_kind != 2 || L.cout_p != 64) return fail(KPD_EINVAL, "fused final layer needs the 64-channel conv");
@@ -886,6 +908,9 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
     p->ws_bytes[k] = need;
   }
   carve(p, d, reinterpret_cast<char*>(p->ws[k]), p->work[k]);
+  // zero once: the padded heatmap-conv maps keep their zero border (the
+  // kernels write interiors only)
+  if (hm_padded(p)) HIP_TRY(hipMemsetAsync(p->ws[k], 0, need, st));
   p->dims[k] = d;
   p->have_work[k] = true;
   return KPD_OK;
@@ -1155,20 +1180,20 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw, st));
   HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
   const bool bf = p->precision == KPD_PRECISION_MIXED;
-  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, bf ? 1 : 0, st));
+  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, bf ? (hm_padded(p) ? 2 : 1) : 0, st));
   att_stage.reset();
   std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
-  if (int rc = hm_conv(p->hm1, w.xs, R, 64, w.h1, 1, st)) return rc;
+  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st)) return rc;
   c1.reset();
   std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
-  if (int rc = hm_conv(p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st)) return rc;
+  if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st)) return rc;
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
   // mixed: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
   static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
   const bool fin_fused = p->hm3.bf16 && p->hm3.cout_p == 64 && !no_fin_fuse;
   const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
-  if (int rc = hm_conv(p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr)) return rc;
+  if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr)) return rc;
   c3.reset();
   {
     Stage sg(p, "hm_final_decode", st);
