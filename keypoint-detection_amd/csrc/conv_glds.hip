@@ -75,6 +75,12 @@ __device__ __forceinline__ void glds16(i32x4 rsrc, unsigned lds_dst, unsigned vo
       : "memory");
 }
 
+// diagnostic phase stamps (KPD_STAMPS): thread 0 records s_memrealtime
+__device__ __forceinline__ void stamp16(unsigned long long* st, int i, unsigned long long v = 0, int row = -1) {
+  if (st && threadIdx.x == 0)
+    st[(size_t)(row < 0 ? blockIdx.x : row) * 8 + i] = v ? v : __builtin_amdgcn_s_memrealtime();
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt");
@@ -572,7 +578,9 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
   constexpr int A_LD = 4, B_LD = BN / 64, LPT = A_LD + B_LD;
   constexpr int STAGE = (BM + BN) * ROWB, RING = S * STAGE;
-  constexpr int LDS = RING + 2 * WAVES_M * BN * 4;
+  // ring | stats exchange [2][WAVES_M][BN] | bias [BN] | class tables (ng, woff, g[4]) x 16
+  constexpr int SMISC = RING + 2 * WAVES_M * BN * 4;
+  constexpr int LDS = SMISC + BN * 4 + 16 * 6 * 4;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   constexpr int KT0 = 5;                          // tap0 K-tiles: taps (2k, 2k+1)
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -580,15 +588,18 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int Hf = p.Hf, Wf = p.Wf, rh = p.rh, rw = p.rw, RG = rh * rw;
-  // tile order: position class fastest, so the 16 classes of one (image, row
-  // block) -- which read the same tap0 / lateral-1 pixels -- run back to back
-  // on one XCD (xcd_remap) and share its L2
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int cls = L & 15, nj = L >> 4, n = nj / p.tpc, jt = nj - n * p.tpc;
-  const int ca = cls >> 2, cb = cls & 3;
-  const int q0 = jt * BM;                         // first lat1-grid pixel of the tile
-  const int NG = p.cls_ng[cls];
-  const int KT = KT0 + 4 * NG;
+  // Persistent: one workgroup per CU walks rounds k = 0, 1, ... of the tile
+  // space; in round k it takes logical tile k*G + (rb + k) % G.  Within a
+  // round the tiles of one XCD are consecutive (xcd_remap) and the position
+  // class is fastest, so the 16 classes of an (image, row block) -- which read
+  // the same tap0 / lateral-1 pixels -- run together on one XCD and share its
+  // L2; the (rb + k) rotation walks every workgroup through the classes, so
+  // the per-class K-tile counts (9 / 13 / 21) balance out.  The next tile's
+  // first K-tiles are issued right after the K loop, so their LDS-DMA
+  // latency overlaps this tile's epilogue.
+  const int ntiles = 16 * p.N * p.tpc, G = gridDim.x;
+  const int rb = xcd_remap(blockIdx.x, G);
+  auto tile_at = [&](int k) { return k * G + (rb + k) % G; };
 
   const i32x4 rf = make_rsrc(p.f_split, p.f_bytes), rl = make_rsrc(p.l_split, p.l_bytes);
   const i32x4 rw0 = make_rsrc(p.w0, p.w0_bytes), rwe = make_rsrc(p.weff, p.weff_bytes);
@@ -596,36 +607,71 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   const unsigned a_dst = __builtin_amdgcn_readfirstlane(lds0 + wave * 32 * ROWB);
   const unsigned b_dst = __builtin_amdgcn_readfirstlane(lds0 + (BM + wave * (BN / 8)) * ROWB);
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
-
-  // per staged row: tap0 pixel offset (64-byte rows) + 9-tap mask, lat1 pixel
-  // offset (512-byte rows) + group mask
-  unsigned f_off[A_LD], f_mask[A_LD], l_off[A_LD], l_mask[A_LD];
+  // once per workgroup: the unscale of the split products (a kernel-wide
+  // constant), the bias and the per-class tables in LDS (the per-tile setup
+  // then reads LDS instead of dependent kernel-argument loads)
+  float* s_bias = reinterpret_cast<float*>(lds + SMISC);
+  int* s_ng = reinterpret_cast<int*>(lds + SMISC + BN * 4);
+  int* s_woff = s_ng + 16;
+  int* s_g = s_ng + 32;   // [16][4]
+  if (tid < BN) s_bias[tid] = p.bias[tid];
+  if (tid < 16) {
+    s_ng[tid] = p.cls_ng[tid];
+    s_woff[tid] = p.cls_woff[tid];
 #pragma unroll
-  for (int i = 0; i < A_LD; ++i) {
-    const int q = q0 + wave * 32 + i * 8 + lrow;
-    f_off[i] = l_off[i] = 0;
-    f_mask[i] = l_mask[i] = 0;
-    if (q < RG) {
-      const int Y = q / rw, X = q - Y * rw, y = 4 * Y + ca, x = 4 * X + cb;
-      f_off[i] = (unsigned)((((size_t)n * Hf + y) * Wf + x) * 64);
-      l_off[i] = (unsigned)((((size_t)n * rh + Y) * rw + X) * 512);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy >= 0 && yy < Hf && xx >= 0 && xx < Wf) f_mask[i] |= 1u << t;
-      }
-      for (int g = 0; g < NG; ++g) {
-        const int gg = p.cls_g[cls][g], oy = gg / 3 - 1, ox = gg % 3 - 1;
-        if (Y + oy >= 0 && Y + oy < rh && X + ox >= 0 && X + ox < rw) l_mask[i] |= 1u << g;
-      }
-    }
+    for (int gi = 0; gi < kFpn0xMaxGroups; ++gi) s_g[tid * 4 + gi] = p.cls_g[tid][gi];
   }
+  float scale;
+  {
+    int a_f, a_l, P;
+    fpn0x_exps_from(fpn0x_slots(p.sc), p.w_exp0, p.w_expE, &a_f, &a_l, &P);
+    scale = ldexpf(1.f, -P);
+  }
+  __syncthreads();
   // this lane's 16-byte piece of a tap0 K-row: chunks 0-1 hi(t1), 2-3 hi(t2),
   // 4-5 lo(t1), 6-7 lo(t2); a tap0 pixel row is [hi16 | lo16] (64 bytes)
   const int f_tsel = (lchunk >> 1) & 1;                       // 0: t1, 1: t2
   const unsigned f_byte = (unsigned)((lchunk >> 2) * 32 + (lchunk & 1) * 16);
   const int co_b = wave * (BN / 8) + lrow;                     // B rows of this lane (+ 8 i)
-  int ld = 0;                                                  // next K-tile to issue
+
+  // per-tile state
+  int cls = 0, n = 0, jt = 0, ca = 0, cb = 0, q0 = 0, NG = 1, KT = 0, ld = 0;
+  // masks packed: bits 0-8 = tap0 taps in the image, bits 9-12 = lat1 groups in the grid
+  unsigned f_off[A_LD], l_off[A_LD], mask[A_LD];
+  auto setup = [&](int L) {
+    cls = L & 15;
+    const int nj = L >> 4;
+    n = nj / p.tpc;
+    jt = nj - n * p.tpc;
+    ca = cls >> 2;
+    cb = cls & 3;
+    q0 = jt * BM;                                  // first lat1-grid pixel of the tile
+    NG = s_ng[cls];
+    KT = KT0 + 4 * NG;
+    ld = 0;
+    // per staged row: tap0 pixel offset (64-byte rows) + 9-tap mask, lat1
+    // pixel offset (512-byte rows) + group mask
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int q = q0 + wave * 32 + i * 8 + lrow;
+      f_off[i] = l_off[i] = 0;
+      mask[i] = 0;
+      if (q < RG) {
+        const int Y = q / rw, X = q - Y * rw, y = 4 * Y + ca, x = 4 * X + cb;
+        f_off[i] = (unsigned)((((size_t)n * Hf + y) * Wf + x) * 64);
+        l_off[i] = (unsigned)((((size_t)n * rh + Y) * rw + X) * 512);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+          if (yy >= 0 && yy < Hf && xx >= 0 && xx < Wf) mask[i] |= 1u << t;
+        }
+        for (int g = 0; g < NG; ++g) {
+          const int gg = s_g[cls * 4 + g], oy = gg / 3 - 1, ox = gg % 3 - 1;
+          if (Y + oy >= 0 && Y + oy < rh && X + ox >= 0 && X + ox < rw) mask[i] |= 1u << (9 + g);
+        }
+      }
+    }
+  };
   auto issue = [&](int stage) {
     const unsigned so = stage * STAGE;
     if (ld < KT0) {
@@ -634,7 +680,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
       const int delta = (dy * Wf + dx) * 64 + (int)f_byte;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const unsigned voff = (t < 9 && ((f_mask[i] >> t) & 1u)) ? f_off[i] + delta : OOB;
+        const unsigned voff = (t < 9 && ((mask[i] >> t) & 1u)) ? f_off[i] + delta : OOB;
         glds16(rf, a_dst + so + i * 8 * ROWB, voff, 0);
       }
 #pragma unroll
@@ -642,14 +688,14 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         glds16(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + ld) * ROWB + lchunk * 16), 0);
     } else {
       const int k = ld - KT0, g = k >> 2, kc = k & 3;
-      const int gg = p.cls_g[cls][g], oy = gg / 3 - 1, ox = gg % 3 - 1;
+      const int gg = s_g[cls * 4 + g], oy = gg / 3 - 1, ox = gg % 3 - 1;
       const int delta = (oy * rw + ox) * 512 + kc * 128 + lchunk * 16;
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
-        const unsigned voff = ((l_mask[i] >> g) & 1u) ? l_off[i] + delta : OOB;
+        const unsigned voff = ((mask[i] >> (9 + g)) & 1u) ? l_off[i] + delta : OOB;
         glds16(rl, a_dst + so + i * 8 * ROWB, voff, 0);
       }
-      const int wbase = p.cls_woff[cls] * 2;   // bytes
+      const int wbase = s_woff[cls] * 2;   // bytes
 #pragma unroll
       for (int i = 0; i < B_LD; ++i)
         glds16(rwe, b_dst + so + i * 8 * ROWB,
@@ -659,49 +705,38 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   };
 
   f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, r16 = lane & 15;
   const int a_row = (wm * WM + r16) * ROWB, b_row = (BM + wn * 64 + r16) * ROWB;
   const int ch0 = ((g ^ (r16 & 7)) << 4), ch1 = (((4 + g) ^ (r16 & 7)) << 4);
-  struct Frag {
-    uint4 a[2][FM], b[2][FN];
-  };
-  auto load_frags = [&](int stage, Frag& f) {
+  // One fragment set: a0/a1 (hi/lo of A), b0/b1 (hi/lo of B).  The three
+  // product passes of K-tile k run as a1.b0 | a0.b1 | a0.b0, and each
+  // register group is refilled with tile k+1 as soon as its last pass of
+  // tile k has issued (a1 after pass 1, b1 after pass 2, a0 / b0 after pass
+  // 3): the reads of the next tile overlap the MFMAs of this one with half
+  // the registers of a double-buffered set (no spills beside the persistent
+  // loop's next-tile state).
+  uint4 fa0[FM], fa1[FM], fb0[FN], fb1[FN];
+  auto rd_a = [&](int stage, int hl, uint4* f) {
     const char* sb = lds + stage * STAGE;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      f.a[0][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch0);
-      f.a[1][i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + ch1);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      f.b[0][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch0);
-      f.b[1][j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + ch1);
-    }
+    for (int i = 0; i < FM; ++i) f[i] = *reinterpret_cast<const uint4*>(sb + a_row + i * 16 * ROWB + (hl ? ch1 : ch0));
   };
-  auto mma = [&](const Frag& f) {
+  auto rd_b = [&](int stage, int hl, uint4* f) {
+    const char* sb = lds + stage * STAGE;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
-                                                           __builtin_bit_cast(f16x8, f.b[1][j]), acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[1][i]),
-                                                           __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, f.a[0][i]),
-                                                           __builtin_bit_cast(f16x8, f.b[0][j]), acc[i][j], 0, 0, 0);
+    for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + (hl ? ch1 : ch0));
   };
+  auto pass = [&](const uint4* a, const uint4* b) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, b[j]),
+                                                           acc[i][j], 0, 0, 0);
+  };
+  // the DMAs of K-tile k landed: every DMA younger than it belongs to the
+  // (S-2) later K-tiles, or is a store of the previous tile's epilogue
+  // (stores are counted in vmcnt too: they can only make this wait longer)
   auto tile_ready = [&](int k) {
     if (k + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
     else wait_vmcnt<0>();
@@ -710,93 +745,126 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     asm volatile("" ::: "memory");
   };
 
+  int L = tile_at(0);
+  if (L >= ntiles) return;
+  setup(L);
 #pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < KT) issue(s);
-  {
-    Frag f0, f1;
-    tile_ready(0);
-    load_frags(0, f0);
-    int is = S - 1, rs = 1;
-    auto step = [&](int kt, Frag& cur, Frag& nxt) {
-      if (kt + S - 1 < KT) issue(is);
-      is = is + 1 == S ? 0 : is + 1;
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      if (kt + 1 < KT) {
-        tile_ready(kt + 1);
-        load_frags(rs, nxt);
-        rs = rs + 1 == S ? 0 : rs + 1;
-      }
-      __builtin_amdgcn_s_setprio(1);
-      mma(cur);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    int kt = 0;
-    for (; kt + 1 < KT; kt += 2) {
-      step(kt, f0, f1);
-      step(kt + 1, f1, f0);
-    }
-    if (kt < KT) step(kt, f0, f1);
-  }
-  __syncthreads();
-
-  // ---------------- register epilogue ----------------
-  int a_f, a_l, P;
-  fpn0x_exps(p.sc, p.w_exp0, p.w_expE, &a_f, &a_l, &P);
-  const float scale = ldexpf(1.f, -P);
-  const int t4 = lane & 3, q4 = r16 >> 2;
-  float* sts = reinterpret_cast<float*>(lds + RING);
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = wn * 64 + j * 16;
-    const float bj = p.bias[col + r16];
-    float sm = 0.f, mx = -INFINITY;
+  for (int s2 = 0; s2 < S - 1; ++s2)
+    if (s2 < KT) issue(s2);
+  for (int round = 0; L < ntiles; ++round) {
+    stamp16(p.stamps, 0, 0, L);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
-        acc[i][j][e] = v;
-        const bool row_ok = q0 + wm * WM + i * 16 + g * 4 + e < RG;
-        sm += row_ok ? v : 0.f;
-        mx = row_ok ? fmaxf(mx, v) : mx;
-      }
-    sm += __shfl_xor(sm, 16);
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    sm += __shfl_xor(sm, 32);
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    if (g == 0) {
-      sts[wm * BN + col + r16] = sm;
-      sts[(WAVES_M + wm) * BN + col + r16] = mx;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (tid < BN) {
-    float sm = sts[tid], mx = sts[WAVES_M * BN + tid];
-#pragma unroll
-    for (int w = 1; w < WAVES_M; ++w) {
-      sm += sts[w * BN + tid];
-      mx = fmaxf(mx, sts[(WAVES_M + w) * BN + tid]);
-    }
-    float* st = p.stats + ((size_t)n * 16 * p.tpc + cls * p.tpc + jt) * 2 * BN;
-    st[tid] = sm;
-    st[BN + tid] = mx;
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      f32x4 v = acc[i][j];
-      quad_transpose(v, t4);
-      const int q = q0 + wm * WM + i * 16 + g * 4 + t4;
-      if (q < RG) {
-        const int Y = q / rw, X = q - Y * rw;
-        float* dst = p.out + (((size_t)n * Hf + 4 * Y + ca) * Wf + 4 * X + cb) * BN + wn * 64 + j * 16 + q4 * 4;
-        *reinterpret_cast<f32x4*>(dst) = v;
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      tile_ready(0);
+      stamp16(p.stamps, 1, 0, L);
+      rd_a(0, 1, fa1); rd_b(0, 0, fb0); rd_b(0, 1, fb1); rd_a(0, 0, fa0);
+      int is = S - 1, rs = 0;   // stage the next issue writes / stage of the current tile
+      for (int kt = 0; kt < KT; ++kt) {
+        if (kt + S - 1 < KT) issue(is);   // into the stage of tile kt-1 (free since barrier kt)
+        is = is + 1 == S ? 0 : is + 1;
+        const int ns = rs + 1 == S ? 0 : rs + 1;
+        const bool more = kt + 1 < KT;
+        __builtin_amdgcn_s_setprio(1);
+        pass(fa1, fb0);
+        __builtin_amdgcn_s_setprio(0);
+        if (more) {
+          tile_ready(kt + 1);
+          rd_a(ns, 1, fa1);
+        }
+        __builtin_amdgcn_s_setprio(1);
+        pass(fa0, fb1);
+        __builtin_amdgcn_s_setprio(0);
+        if (more) rd_b(ns, 1, fb1);
+        __builtin_amdgcn_s_setprio(1);
+        pass(fa0, fb0);
+        __builtin_amdgcn_s_setprio(0);
+        if (more) {
+          rd_b(ns, 0, fb0);
+          rd_a(ns, 0, fa0);
+        }
+        rs = ns;
       }
     }
+    __syncthreads();   // every wave's fragment reads of the ring retired: the ring is free
+    stamp16(p.stamps, 2, 0, L);
+    stamp16(p.stamps, 5, (unsigned long long)KT, L);
+    // this tile's geometry for the epilogue; then the next tile's prologue
+    const int e_cls = cls, e_n = n, e_jt = jt, e_ca = ca, e_cb = cb, e_q0 = q0;
+    const int Lnext = tile_at(round + 1);
+    if (Lnext < ntiles) {
+      setup(Lnext);
+#pragma unroll
+      for (int s2 = 0; s2 < S - 1; ++s2)
+        if (s2 < KT) issue(s2);
+    }
+
+    // ---------------- register epilogue ----------------
+    const int t4 = lane & 3, q4 = r16 >> 2;
+    float* sts = reinterpret_cast<float*>(lds + RING);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * 64 + j * 16;
+      const float bj = s_bias[col + r16];
+      float sm = 0.f, mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
+          acc[i][j][e] = v;
+          const bool row_ok = e_q0 + wm * WM + i * 16 + g * 4 + e < RG;
+          sm += row_ok ? v : 0.f;
+          mx = row_ok ? fmaxf(mx, v) : mx;
+        }
+      sm += __shfl_xor(sm, 16);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      sm += __shfl_xor(sm, 32);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      if (g == 0) {
+        sts[wm * BN + col + r16] = sm;
+        sts[(WAVES_M + wm) * BN + col + r16] = mx;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tid < BN) {
+      float sm = sts[tid], mx = sts[WAVES_M * BN + tid];
+#pragma unroll
+      for (int w = 1; w < WAVES_M; ++w) {
+        sm += sts[w * BN + tid];
+        mx = fmaxf(mx, sts[(WAVES_M + w) * BN + tid]);
+      }
+      float* st = p.stats + ((size_t)e_n * 16 * p.tpc + e_cls * p.tpc + e_jt) * 2 * BN;
+      st[tid] = sm;
+      st[BN + tid] = mx;
+    }
+    stamp16(p.stamps, 3, 0, L);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        f32x4 v = acc[i][j];
+        quad_transpose(v, t4);
+        const int q = e_q0 + wm * WM + i * 16 + g * 4 + t4;
+        if (q < RG) {
+          const int Y = q / rw, X = q - Y * rw;
+          float* dst =
+              p.out + (((size_t)e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + j * 16 + q4 * 4;
+          *reinterpret_cast<f32x4*>(dst) = v;
+        }
+      }
+    if (p.stamps) {   // diagnostic build path: the stores' completion
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp16(p.stamps, 4, 0, L);
+    }
+    // the stats exchange region is rewritten by the next tile only after the
+    // barriers of its K loop
+    L = Lnext;
+  }
 }
 
 // fp32 rows -> f16 hi|lo rows (groups of G = 32 channels, 16 when cin == 16),
@@ -1164,7 +1232,17 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   if (a.N <= 0) return hipSuccess;
   if (a.Hf != 4 * a.rh || a.Wf != 4 * a.rw || a.tpc != (a.rh * a.rw + BM - 1) / BM) return hipErrorInvalidValue;
   const long tiles = 16L * a.N * a.tpc;
-  hipLaunchKernelGGL(fpn0x_kernel, dim3((unsigned)tiles), dim3(NT), 0, st, a);
+  // persistent: one workgroup per CU (the kernel walks the tiles in rounds)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  static const int grid_env = getenv("KPD_FPN0X_GRID") ? atoi(getenv("KPD_FPN0X_GRID")) : 0;   // A/B
+  const long grid = std::min<long>(tiles, grid_env > 0 ? grid_env : ncu);
+  hipLaunchKernelGGL(fpn0x_kernel, dim3((unsigned)grid), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -86,6 +86,19 @@ __device__ __forceinline__ int split_exp_of(float amax) {
   frexpf(u, &e);
   return min(max(14 - e, -100), 100);
 }
+// raw slot values of this lane (issue early, reduce late: fpn0x_exps_from)
+__device__ __forceinline__ float2 fpn0x_slots(const float* sc_in) {
+  const int i = (threadIdx.x & 63) * kAmaxStride;
+  return make_float2(sc_in[i], sc_in[kAmaxSlots * kAmaxStride + i]);
+}
+__device__ __forceinline__ void fpn0x_exps_from(float2 sl, int w_exp0, int w_expE, int* a_f, int* a_l, int* P) {
+  const int ef = split_exp_of(wave_max(sl.x)), el = split_exp_of(wave_max(sl.y));
+  int pp = min(ef + w_exp0, el + w_expE);
+  pp = min(max(pp, -120), 120);
+  *P = pp;
+  *a_f = pp - w_exp0;
+  *a_l = pp - w_expE;
+}
 __device__ __forceinline__ void fpn0x_exps(const float* sc_in, int w_exp0, int w_expE, int* a_f, int* a_l, int* P) {
   const int ef = split_exp_of(amax_read(sc_in)), el = split_exp_of(amax_read(sc_in + kAmaxSlots * kAmaxStride));
   int pp = min(ef + w_exp0, el + w_expE);

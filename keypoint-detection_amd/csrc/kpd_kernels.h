@@ -97,6 +97,7 @@ struct Fpn0xArgs {
   const float* sc;         // amax slots: max|tap0|, max|lat1|
   int N, Hf, Wf, rh, rw, tpc, w_exp0, w_expE;
   int f_bytes, l_bytes, w0_bytes, weff_bytes;
+  unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
 // fp32 NHWC -> f16 hi|lo split rows (groups of 32 channels, or 16 for cin 16)

@@ -1123,6 +1123,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     a.f_bytes = (int)std::min<size_t>((size_t)B * lh[0] * lw[0] * 64, 0x7fffffff);
     a.l_bytes = (int)std::min<size_t>((size_t)B * lh[1] * lw[1] * 512, 0x7fffffff);
     a.w0_bytes = p->fpn0x.w0_bytes; a.weff_bytes = p->fpn0x.weff_bytes;
+    a.stamps = take_stamps("stamps_fpn0x", (size_t)16 * B * tpc);
     HIP_TRY(launch_fpn0x(a, st));
   } else if (split) {
     Conv16Args a{};
