@@ -15,6 +15,7 @@
 
 #include "kpd_common.h"
 #include "kpd_kernels.h"
+#include "kpd_dma.h"
 
 namespace {
 
@@ -243,7 +244,7 @@ template <int K, int S, int NTC, int XT, int KC>
 __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
-  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = CS + 4, DA = KC <= 3 ? 4 : 2;
+  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = CS + 4, DA = KC <= 3 ? 4 : 1;
   const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, cin_p = p.cin_p;
   float* es = sm;                                  // [Pin][ESTR]
@@ -281,27 +282,23 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       const int i = tid + u * 256, t = i / CQ, q = i - t * CQ;
       if (i < K * K * CQ) v[u] = *reinterpret_cast<const float4*>(p.wd + (size_t)t * p.Ep + c0 + q * 4);
     }
-    constexpr int NJ = (144 * CQ + 255) / 256;   // sq <= 144 (launch check)
-    float4 v1[NJ];
+    // the fc1 columns by LDS-DMA (no registers; waited for after the expand):
+    // 16-byte piece e of w1s = [sq][CS] is w1[j][c0 + 4 q], e = j * CQ + q,
+    // padding channels (>= C) load zeros through the range check
     if (p.part) {
-#pragma unroll
-      for (int u = 0; u < NJ; ++u) {
-        const int i = tid + u * 256, j = i / CQ, q = i - j * CQ;
-        v1[u] = (i < p.sq * CQ && c0 + q * 4 < p.C)
-                    ? *reinterpret_cast<const float4*>(p.w1 + (size_t)j * p.C + c0 + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const i32x4 rw1 = make_rsrc(p.w1, p.sq * p.C * 4);
+      const unsigned w1s_lds = lds_addr(w1s);
+      const int npc = (p.sq * CQ + 63) / 64;   // wave-instructions (1 KiB each)
+      for (int i = wave; i < npc; i += 4) {
+        const int e = i * 64 + lane, j = e / CQ, q = e - j * CQ;
+        const unsigned voff = (j < p.sq && c0 + q * 4 < p.C) ? (unsigned)((j * p.C + c0 + q * 4) * 4) : 0x80000000u;
+        glds16(rw1, __builtin_amdgcn_readfirstlane(w1s_lds + i * 1024), voff, 0);
       }
     }
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
       const int i = tid + u * 256;
       if (i < K * K * CQ) reinterpret_cast<float4*>(wds)[i] = v[u];
-    }
-    if (p.part) {
-#pragma unroll
-      for (int u = 0; u < NJ; ++u) {
-        const int i = tid + u * 256;
-        if (i < p.sq * CQ) reinterpret_cast<float4*>(w1s)[i] = v1[u];
-      }
     }
   }
   stamp(p.stamps, 1);
@@ -342,6 +339,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       }
     }
   }
+  if (p.part) wait_vmcnt<0>();   // the fc1-column DMA (issued at the start; long landed)
   __syncthreads();
   stamp(p.stamps, 2);
   // depthwise from LDS, XT consecutive output columns per thread (input
@@ -1139,14 +1137,16 @@ hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st) {
 
 size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
-  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)K * K * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) +
-                      (a.part ? (size_t)a.sq * a.CS : 0);
+  // the fc1 columns are filled by 1 KiB LDS-DMA pieces: round up to whole pieces
+  const size_t w1f = a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
+  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)K * K * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
   return 4 * main;
 }
 
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
   const int kc = a.cin_p / 16;
-  if ((a.CS != 16 && a.CS != 32) || a.Ep % a.CS || a.cin_p % 16 || (kc != 2 && kc != 3 && kc != 6) || !a.we ||
+  if ((a.CS != 16 && a.CS != 32 && a.CS != 48) || a.Ep % a.CS || a.cin_p % 16 || (kc != 2 && kc != 3 && kc != 6) ||
+      !a.we ||
       (a.part && (!a.pooled || !a.w1 || a.sq <= 0 || a.sq > 144 || a.C % 4)))
     return hipErrorInvalidValue;
   const size_t lds = exdw_lds_bytes(a, K);
@@ -1164,9 +1164,11 @@ hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
     if (a.CS == 16) {                                   \
       if (xt4) EXDW_KC(KK, SS, 1, 4);                   \
       else EXDW_KC(KK, SS, 1, 2);                       \
-    } else {                                            \
+    } else if (a.CS == 32) {                            \
       if (xt4) EXDW_KC(KK, SS, 2, 4);                   \
       else EXDW_KC(KK, SS, 2, 2);                       \
+    } else {                                            \
+      EXDW_KC(KK, SS, 3, 2);                            \
     }                                                   \
   } while (0)
   if (K == 3 && S == 1) EXDW(3, 1);

@@ -1011,6 +1011,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       // slice width fixed per layer (never per batch: the fc1 partial sums
       // must not depend on what an image is batched with)
       static const int cs_env = getenv("KPD_EXDW_CS") ? atoi(getenv("KPD_EXDW_CS")) : 0;   // A/B sweeps
+      // 32 channels from 288 expanded channels up, else 16 (48 for the
+      // 576-wide blocks measured slower: 188 VGPRs, 30 vs 23 us)
       xa.CS = cs_env > 0 ? cs_env : (bn.dw.Cp >= 288 ? 32 : 16);
       fused = bn.dw.Cp % xa.CS == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 160 * 1024;
     }
