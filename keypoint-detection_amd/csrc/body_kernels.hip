@@ -647,6 +647,158 @@ __global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, floa
   }
 }
 
+// The narrow SE block without expand (features.1 of mobilenet_v3_small:
+// 16 -> 16 channels, depthwise 3x3 stride 2 + ReLU, SE 16 -> 8 -> 16,
+// project 1x1, no residual; torchvision InvertedResidual via backbone.py:
+// 250-254) in two launches instead of three:
+//   dwsum_kernel: depthwise on tiles of TH output rows x the full width of one
+//     image, plus the tile's per-channel sums (fixed order) for the squeeze;
+//   se16_proj_kernel: the excitation from those partial sums (every workgroup
+//     recomputes it: 16 x 8 x 2 MACs) and the project 1x1 with the excitation
+//     applied to its input, one pixel per thread.
+constexpr int kDwsTH = 4;   // output rows per dwsum workgroup
+template <int K, int S>
+__global__ __launch_bounds__(256) void dwsum_kernel(const float* __restrict__ in, int Hi, int Wi,
+                                                    const float* __restrict__ w, const float* __restrict__ b, int act,
+                                                    float* __restrict__ out, int Ho, int Wo,
+                                                    float* __restrict__ part) {
+  constexpr int C = 16, CQ = 4, XT = 4, P = (K - 1) / 2, NC = (XT - 1) * S + K;
+  __shared__ float4 red[256];
+  const int n = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
+  const int wx = (Wo + XT - 1) / XT, units = kDwsTH * wx * CQ;
+  const int q = tid % CQ, rest = tid / CQ, xt = rest % wx, orow = rest / wx;
+  const int oy = tile * kDwsTH + orow, ox0 = xt * XT, ix0 = ox0 * S - P;
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < units && oy < Ho) {
+    float4 acc[XT];
+#pragma unroll
+    for (int o = 0; o < XT; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // row by row (36 VGPRs of inputs): occupancy hides the load latency
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const int iy = oy * S - P + ky;
+      if (iy < 0 || iy >= Hi) continue;
+      float4 col[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ix = ix0 + c;
+        col[c] = (ix >= 0 && ix < Wi) ? *reinterpret_cast<const float4*>(in + (((size_t)n * Hi + iy) * Wi + ix) * C + q * 4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        const float4 k4 = *reinterpret_cast<const float4*>(w + (ky * K + kx) * C + q * 4);
+#pragma unroll
+        for (int o = 0; o < XT; ++o) {
+          const float4 v = col[o * S + kx];
+          acc[o].x = fmaf(v.x, k4.x, acc[o].x); acc[o].y = fmaf(v.y, k4.y, acc[o].y);
+          acc[o].z = fmaf(v.z, k4.z, acc[o].z); acc[o].w = fmaf(v.w, k4.w, acc[o].w);
+        }
+      }
+    }
+    const float4 bb = *reinterpret_cast<const float4*>(b + q * 4);
+    float* op = out + (((size_t)n * Ho + oy) * Wo + ox0) * C + q * 4;
+#pragma unroll
+    for (int o = 0; o < XT; ++o) {
+      if (ox0 + o >= Wo) break;
+      float4 r;
+      r.x = kpd_act(acc[o].x + bb.x, act); r.y = kpd_act(acc[o].y + bb.y, act);
+      r.z = kpd_act(acc[o].z + bb.z, act); r.w = kpd_act(acc[o].w + bb.w, act);
+      *reinterpret_cast<float4*>(op + (size_t)o * C) = r;
+      sum.x += r.x; sum.y += r.y; sum.z += r.z; sum.w += r.w;
+    }
+  }
+  // tile channel sums: the 16 lanes of a wave that share a quad (lane bits
+  // 2-5) by xor shuffles, then the 4 waves in order (fixed order throughout)
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {
+    sum.x += __shfl_xor(sum.x, o); sum.y += __shfl_xor(sum.y, o);
+    sum.z += __shfl_xor(sum.z, o); sum.w += __shfl_xor(sum.w, o);
+  }
+  if ((tid & 63) < CQ) red[(tid >> 6) * CQ + (tid & 63)] = sum;
+  __syncthreads();
+  if (tid < C) {
+    const int cq = tid >> 2, e = tid & 3;
+    float t = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) {
+      const float4 v = red[wv * CQ + cq];
+      t += e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+    }
+    part[((size_t)n * gridDim.x + tile) * C + tid] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict__ d, int npx, int ntiles,
+                                                        const float* __restrict__ part, const float* __restrict__ w1,
+                                                        const float* __restrict__ b1, const float* __restrict__ w2t,
+                                                        const float* __restrict__ b2, int sq,
+                                                        const float* __restrict__ wp, const float* __restrict__ bp,
+                                                        float* __restrict__ out) {
+  constexpr int C = 16;
+  __shared__ float mean[C], hid[16], sc[C], wps[C * C], bps[C];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  const int px = blockIdx.x * 256 + tid;
+  // this thread's pixel first (its latency overlaps the excitation)
+  float4 v[4];
+  const bool live = px < npx;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    v[k] = reinterpret_cast<const float4*>(d + ((size_t)n * npx + min(px, npx - 1)) * C)[k];
+  // the image's tile partials (ntiles x 16 <= 1024 floats) staged in one load
+  // round trip, then summed in tile order
+  __shared__ float sp[1024];
+  {
+    const float* pp = part + (size_t)n * ntiles * C;
+    float t4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t4[u] = pp[min(tid + u * 256, ntiles * C - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * 256 < ntiles * C) sp[tid + u * 256] = t4[u];
+  }
+  if (tid < C * C) wps[tid] = wp[tid];
+  if (tid < C) bps[tid] = bp[tid];
+  __syncthreads();
+  if (tid < C) {
+    float t = 0.f;
+    for (int i = 0; i < ntiles; ++i) t += sp[i * C + tid];
+    mean[tid] = t / (float)npx;
+  }
+  __syncthreads();
+  if (tid < sq) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) a = fmaf(w1[tid * C + c], mean[c], a);
+    hid[tid] = fmaxf(a + b1[tid], 0.f);
+  }
+  __syncthreads();
+  if (tid < C) {
+    float a = 0.f;
+    for (int j = 0; j < sq; ++j) a = fmaf(w2t[j * C + tid], hid[j], a);
+    sc[tid] = kpd_hsigmoid(a + b2[tid]);
+  }
+  __syncthreads();
+  if (!live) return;
+  float x[C];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[4 * k] = v[k].x * sc[4 * k]; x[4 * k + 1] = v[k].y * sc[4 * k + 1];
+    x[4 * k + 2] = v[k].z * sc[4 * k + 2]; x[4 * k + 3] = v[k].w * sc[4 * k + 3];
+  }
+  float o[C];
+#pragma unroll
+  for (int co = 0; co < C; ++co) {
+    float a = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) a = fmaf(x[c], wps[co * C + c], a);
+    o[co] = a + bps[co];
+  }
+  float4* op = reinterpret_cast<float4*>(out + ((size_t)n * npx + px) * C);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) op[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+}
+
 // Fused MobileNetV3 inverted residual without SE (features.2 / features.3 of
 // mobilenet_v3_small, backbone.py:250-254): expand 1x1 + act, depthwise KxK
 // stride S + act, project 1x1 (+ residual), on a tile of TH output rows x the
@@ -1204,6 +1356,26 @@ hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
   else if (mt == 12 && ntt == 3) SEP(12, 3);
   else return hipErrorInvalidValue;
 #undef SEP
+  return hipGetLastError();
+}
+
+hipError_t launch_dwsum(const float* in, int N, int Hi, int Wi, const float* w, const float* b, int act, float* out,
+                         int Ho, int Wo, int k, int s, float* part, int* ntiles, hipStream_t st) {
+  if (kDwsTH * ((Wo + 3) / 4) * 4 > 256) return hipErrorInvalidValue;
+  const dim3 grid((Ho + kDwsTH - 1) / kDwsTH, N);
+  *ntiles = (int)grid.x;
+  if (k == 3 && s == 2) hipLaunchKernelGGL((dwsum_kernel<3, 2>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
+  else if (k == 3 && s == 1) hipLaunchKernelGGL((dwsum_kernel<3, 1>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_se16_proj(const float* d, int N, int npx, int ntiles, const float* part, const float* w1,
+                            const float* b1, const float* w2t, const float* b2, int sq, const float* wp,
+                            const float* bp, float* out, hipStream_t st) {
+  if (sq > 16 || ntiles * 16 > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(se16_proj_kernel, dim3((npx + 255) / 256, N), dim3(256), 0, st, d, npx, ntiles, part, w1, b1, w2t,
+                     b2, sq, wp, bp, out);
   return hipGetLastError();
 }
 

@@ -173,6 +173,13 @@ struct SeProjArgs {
 };
 size_t seproj_lds_bytes(const SeProjArgs& a);
 hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st);
+// features.1 (16 channels, no expand): depthwise + per-tile channel sums, then
+// excitation + project (body_kernels.hip, dwsum_kernel / se16_proj_kernel)
+hipError_t launch_dwsum(const float* in, int N, int Hi, int Wi, const float* w, const float* b, int act, float* out,
+                         int Ho, int Wo, int k, int s, float* part, int* ntiles, hipStream_t st);
+hipError_t launch_se16_proj(const float* d, int N, int npx, int ntiles, const float* part, const float* w1,
+                            const float* b1, const float* w2t, const float* b2, int sq, const float* wp,
+                            const float* bp, float* out, hipStream_t st);
 // the excitation alone, for the wide blocks: sesc [N][Ep]
 hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,

@@ -988,6 +988,19 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     // KPD_FIR_MASK (bit i = block i) overrides for A/B runs.
     static const int fir_mask = getenv("KPD_FIR_MASK") ? atoi(getenv("KPD_FIR_MASK")) : -1;
     const bool fir_on = fir_mask < 0 ? bn.cfg.s == 2 : ((fir_mask >> i) & 1) != 0;
+    // features.1: 16 channels, no expand, SE -> depthwise + tile sums, excitation + project
+    static const bool no_f1 = getenv("KPD_NO_F1") != nullptr;   // A/B switch
+    if (!no_f1 && !bn.has_exp && bn.cfg.se && bn.dw.Cp == 16 && bn.cfg.cout == 16 && bn.project.cout_p == 16 &&
+        bn.project.cin_p == 16 && bn.project.k == 1 && !bn.project.bf16 && bn.se.sq <= 16 && bn.dw.k == 3 &&
+        !(bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout) && 4 * ((wo + 3) / 4) * 4 <= 256) {
+      int nt = 0;
+      HIP_TRY(launch_dwsum(x, B, hi, wi, bn.dw.w, bn.dw.b, bn.dw.act, w.d[i], ho, wo, bn.dw.k, bn.dw.s, w.separt, &nt,
+                           st));
+      HIP_TRY(launch_se16_proj(w.d[i], B, ho * wo, nt, w.separt, bn.se.w1, bn.se.b1, bn.se.w2, bn.se.b2, bn.se.sq,
+                               static_cast<const float*>(bn.project.w), bn.project.b, w.o[i], st));
+      x = w.o[i];
+      continue;
+    }
     if (!no_fuse && fir_on && !bn.cfg.se && bn.has_exp && bn.expand.cout_p == bn.dw.Cp &&
         bn.project.cin_p == bn.dw.Cp) {
       FirArgs fa{};

@@ -13,7 +13,7 @@ def main(path):
     if not path.endswith(".csv"):
         path = glob.glob(path + "/**/*kernel_trace.csv", recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "stem_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "stem_" in r["Kernel_Name"]]
     s, e = idx[-2], idx[-1]
     prev = None
     body = 0.0
