@@ -444,7 +444,9 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
   float* red = hid + 256;            // [4][MP][NT] partial tiles / SE scratch
   stamp(a.stamps, 0);
   const int r = lane & 15, g = lane >> 4;
-  const float* dbase = a.d + (size_t)n * Po * Ep;
+  // rows of this workgroup: [m0, m0 + MP) of the image (blockIdx.z splits M)
+  const int m0 = blockIdx.z * MP, Pr = min(MP, Po - m0);
+  const float* dbase = a.d + ((size_t)n * Po + m0) * Ep;
   const int nkc = Ep / 16, ncw = (nkc - wave + 3) / 4;   // this wave's k chunks: wave + 4 t
   float4 av[D][MT], bv[D][NTT];
   auto load_chunk = [&](int t, float4* a4, float4* b4) {
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int px = mt * 16 + r;
-        a4[mt] = px < Po ? *reinterpret_cast<const float4*>(dbase + (size_t)px * Ep + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a4[mt] = px < Pr ? *reinterpret_cast<const float4*>(dbase + (size_t)px * Ep + k) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int nt = 0; nt < NTT; ++nt) b4[nt] = *reinterpret_cast<const float4*>(a.wp + (size_t)(o0 + nt * 16 + r) * Ep + k);
@@ -568,9 +570,9 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
   stamp(a.stamps, 3);
   // (4) sum the 4 waves in order, bias, residual; 4 channels per thread
   constexpr int NQ = NT / 4;
-  float* out = a.out + (size_t)n * Po * a.cout_p + o0;
-  const float* res = a.res ? a.res + (size_t)n * Po * a.cout_p + o0 : nullptr;
-  for (int i = tid; i < Po * NQ; i += 256) {
+  float* out = a.out + ((size_t)n * Po + m0) * a.cout_p + o0;
+  const float* res = a.res ? a.res + ((size_t)n * Po + m0) * a.cout_p + o0 : nullptr;
+  for (int i = tid; i < Pr * NQ; i += 256) {
     const int px = i / NQ, q = i - px * NQ;
     float4 v = *reinterpret_cast<const float4*>(red + px * NT + q * 4);
 #pragma unroll
@@ -1340,18 +1342,27 @@ size_t seproj_lds_bytes(const SeProjArgs& a) {
 }
 
 hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
-  const int mt = (a.Po + 15) / 16;
+  const int mt_all = (a.Po + 15) / 16;
   if (a.Ep % 16 || a.NT % 16 || a.cout_p % a.NT || a.sq > 144 || a.C > a.Ep || a.C % 4 ||
       (size_t)a.nsl * a.sq > 6 * 256 * 4 || (a.nsl * a.sq) % 4)
     return hipErrorInvalidValue;
-  const size_t lds = seproj_lds_bytes(a);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(a.cout_p / a.NT, N);
+  // the 192-pixel maps split their rows over two workgroups (384 instead of
+  // 192 workgroups at 64 images; each recomputes the cheap excitation)
+  static const int msplit_env = getenv("KPD_SEPROJ_MSPLIT") ? atoi(getenv("KPD_SEPROJ_MSPLIT")) : 2;
+  const int msplit = mt_all == 12 ? std::max(1, msplit_env) : 1;
+  const int mt = (mt_all + msplit - 1) / msplit;
+  SeProjArgs b = a;
+  const size_t lds_m = 4 * ((size_t)a.Ep + 256 + std::max({(size_t)4 * mt * 16 * a.NT, (size_t)a.nsl * a.sq,
+                                                             std::max<size_t>(1, std::min<size_t>(16, 256 / (a.C / 4))) * a.C}));
+  if (lds_m > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(a.cout_p / a.NT, N, msplit);
   const int ntt = a.NT / 16;
-#define SEP(M, T) hipLaunchKernelGGL((seproj_kernel<M, T>), grid, dim3(256), lds, st, a)
+#define SEP(M, T) hipLaunchKernelGGL((seproj_kernel<M, T>), grid, dim3(256), lds_m, st, b)
   if (mt == 3 && ntt == 1) SEP(3, 1);
   else if (mt == 3 && ntt == 2) SEP(3, 2);
   else if (mt == 3 && ntt == 3) SEP(3, 3);
+  else if (mt == 6 && ntt == 1) SEP(6, 1);
+  else if (mt == 4 && ntt == 1) SEP(4, 1);
   else if (mt == 12 && ntt == 1) SEP(12, 1);
   else if (mt == 12 && ntt == 3) SEP(12, 3);
   else return hipErrorInvalidValue;

@@ -887,7 +887,9 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
 //           written to the [B][P][17][56][56] heatmap at the ROI's slot.
 constexpr int HP = 58, HPP = HP * HP;   // padded ROI side, positions per ROI
 constexpr int AWIN = 384;               // A window rows per chunk
-template <int BN, int SB>
+// DBG (A/B ablations, KPD_HMCONV_DBG): 1 = no MFMA, 2 = no weight / window
+// DMA inside the K loop (the prologue's still lands)
+template <int BN, int SB, int DBG = 0>
 __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
@@ -970,6 +972,10 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     for (int i = 0; i < FM; ++i) f.a[i] = *reinterpret_cast<const uint4*>(ab + (r0w + i * 16) * ROWB + ach);
   };
   auto mma_half = [&](const Half& f) {
+    if constexpr ((DBG & 1) != 0) {
+      acc[0][0][0] += __uint_as_float(f.a[0].x ^ f.b[FN - 1].w);   // keep the fragment reads alive
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1007,8 +1013,10 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     if (k + 1 < KT) {
       const int k1 = k + 1, c1 = k1 / 9, t1 = k1 - c1 * 9;
       barrier_k(k1 + SB - 2 >= KT);   // B(k1) and its chunk's window landed; reads of k retired
-      if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);   // next chunk's window, spread over taps
-      if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);         // into the stage of B(k)
+      if constexpr ((DBG & 2) == 0) {
+        if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);   // next chunk's window, spread over taps
+        if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);         // into the stage of B(k)
+      }
       load_half(k1, 0, f0);
     } else {
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1190,7 +1198,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // wider tile halves the weight bytes per MFMA; conv 3 has 64 outputs
     const int bn = fin ? 64 : (a.cout % 256 == 0 ? 256 : 128);
     const dim3 grid((unsigned)(((rows + BM - 1) / BM) * (a.cout / bn)));
+    static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
     if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
+    else if (bn == 256 && dbg == 1) hipLaunchKernelGGL((hmconv_kernel<256, 2, 1>), grid, dim3(NT), 0, st, a);
+    else if (bn == 256 && dbg == 2) hipLaunchKernelGGL((hmconv_kernel<256, 2, 2>), grid, dim3(NT), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2>), grid, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((hmconv_kernel<128, 4>), grid, dim3(NT), 0, st, a);
     const hipError_t e = hipGetLastError();
