@@ -24,38 +24,76 @@ constexpr int TOPK = 64;
 constexpr int FC = 128;             // FPN channels
 
 // ---------------------------------------------------------------- top-k
-// One 128-thread workgroup per image.  stats: [N][tiles][2][128].
-__global__ __launch_bounds__(128) void topk_kernel(const float* __restrict__ stats, int tiles, int HW,
+// ChannelAttention + select_top_k_channels (keypoint_model.py:18-44,
+// 653-661).  One 256-thread workgroup per image.  stats: [N][tiles][2][128]
+// partial channel sums / maxima from the FPN level-0 epilogue.  The image's
+// partials and both FC weights are staged in LDS in one load round trip
+// (every load in flight before the first use); the sums then run in tile
+// order from LDS, as before.
+constexpr int kTopkMaxTiles = 144;   // LDS: tiles x 1 KB + 8 KB
+__global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ stats, int tiles, int HW,
                                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                                    const float* __restrict__ w2, const float* __restrict__ b2,
                                                    int32_t* __restrict__ topk, float* __restrict__ scores_out) {
+  extern __shared__ __attribute__((aligned(16))) float tsm[];
+  // more tiles than fit in LDS (the fp32 path's small tiles at 384x288):
+  // the partials are summed straight from global memory
+  const bool staged = tiles <= kTopkMaxTiles;
+  const int lt = staged ? tiles : 0;
+  float* sst = tsm;                        // [tiles][2][FC]
+  float* sw0 = sst + lt * 2 * FC;          // [8][FC]
+  float* sw2 = sw0 + 8 * FC;               // [FC][8]
   __shared__ float avg[FC], mx[FC], h[16], sc[FC];
-  const int n = blockIdx.x, c = threadIdx.x;
-  const float* st = stats + (size_t)n * tiles * 2 * FC;
-  float s = 0.f, m = -INFINITY;
-  for (int t = 0; t < tiles; ++t) {
-    s += st[t * 2 * FC + c];
-    m = fmaxf(m, st[t * 2 * FC + FC + c]);
+  const int n = blockIdx.x, tid = threadIdx.x, c = tid;
+  {
+    const float4* st4 = reinterpret_cast<const float4*>(stats + (size_t)n * tiles * 2 * FC);
+    const int nst = lt * 2 * FC / 4, nw = 8 * FC / 4, tot = nst + 2 * nw;
+    constexpr int U = 12;   // float4 per thread per pass (one pass up to 40 tiles)
+    for (int base = 0; base < tot; base += U * 256) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + tid + u * 256;
+        v[u] = i < nst ? st4[i]
+             : i < nst + nw ? reinterpret_cast<const float4*>(w0)[i - nst]
+             : i < tot ? reinterpret_cast<const float4*>(w2)[i - nst - nw] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + tid + u * 256;
+        if (i < tot) reinterpret_cast<float4*>(tsm)[i] = v[u];
+      }
+    }
   }
-  avg[c] = s / (float)HW;
-  mx[c] = m;
+  __syncthreads();
+  if (c < FC) {
+    const float* src = staged ? sst : stats + (size_t)n * tiles * 2 * FC;
+    float s = 0.f, m = -INFINITY;
+    for (int t = 0; t < tiles; ++t) {
+      s += src[t * 2 * FC + c];
+      m = fmaxf(m, src[t * 2 * FC + FC + c]);
+    }
+    avg[c] = s / (float)HW;
+    mx[c] = m;
+  }
   __syncthreads();
   if (c < 16) {  // hidden units: 0..7 for avg branch, 8..15 for max branch
     const int j = c & 7;
-    const float* v = (c < 8) ? avg : mx;
+    const float* vv = (c < 8) ? avg : mx;
     float a = b0[j];
-    for (int k = 0; k < FC; ++k) a = fmaf(w0[j * FC + k], v[k], a);
+    for (int k = 0; k < FC; ++k) a = fmaf(sw0[j * FC + k], vv[k], a);
     h[c] = fmaxf(a, 0.f);
   }
   __syncthreads();
+  if (c >= FC) return;
   float oa = b2[c], om = b2[c];
   for (int j = 0; j < 8; ++j) {
-    oa = fmaf(w2[c * 8 + j], h[j], oa);
-    om = fmaf(w2[c * 8 + j], h[8 + j], om);
+    oa = fmaf(sw2[c * 8 + j], h[j], oa);
+    om = fmaf(sw2[c * 8 + j], h[8 + j], om);
   }
   const float score = kpd_sigmoid(oa + om);
   sc[c] = score;
-  __syncthreads();
+  __syncthreads();   // waves 2-3 (c >= 128) have exited: the barrier counts waves 0-1
   // rank = number of channels ordered before c (score desc, index asc on ties)
   int rank = 0;
   for (int k = 0; k < FC; ++k) {
@@ -414,7 +452,8 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
 
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st) {
-  hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(FC), 0, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores);
+  const size_t lds = ((size_t)(tiles <= kTopkMaxTiles ? tiles : 0) * 2 * FC + 2 * 8 * FC) * 4;
+  hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores);
   return hipGetLastError();
 }
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipStream_t st) {
