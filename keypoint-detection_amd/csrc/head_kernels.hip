@@ -299,20 +299,41 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
                                                        int out_bf16) {
   __shared__ float scw[TOPK];
   __shared__ float w[98];
+  __shared__ float2 srow[7][HM + 6];   // the 7 smap rows around y, zero-padded by 3 columns
   const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
-  scw[x] = cw[(size_t)r * TOPK + x];
-  for (int i = x; i < 98; i += 64) w[i] = saw[i];
+  const float* sm = smap + (size_t)r * HMP * 2;
+  {   // every load of the workgroup issued before the first LDS store
+    float2 sv[7];
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      const int iy = y + ky - 3;
+      sv[ky] = (x < HM && iy >= 0 && iy < HM) ? *reinterpret_cast<const float2*>(sm + (iy * HM + x) * 2)
+                                                : make_float2(0.f, 0.f);
+    }
+    const float cwv = cw[(size_t)r * TOPK + x];
+    const float w0v = saw[x], w1v = x + 64 < 98 ? saw[x + 64] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      if (x < HM) srow[ky][x + 3] = sv[ky];
+      if (x < 3) { srow[ky][x] = make_float2(0.f, 0.f); srow[ky][HM + 3 + x] = make_float2(0.f, 0.f); }
+    }
+    scw[x] = cwv;
+    w[x] = w0v;
+    if (x + 64 < 98) w[x + 64] = w1v;
+  }
   __syncthreads();
   if (x >= HM) return;
+  // same tap order (ky, kx) as the reference conv; out-of-image taps add 0
   float a = 0.f;
-  const float* sm = smap + (size_t)r * HMP * 2;
+#pragma unroll
   for (int ky = 0; ky < 7; ++ky) {
     const int iy = y + ky - 3;
     if (iy < 0 || iy >= HM) continue;
+#pragma unroll
     for (int kx = 0; kx < 7; ++kx) {
       const int ix = x + kx - 3;
       if (ix < 0 || ix >= HM) continue;
-      const float2 v = *reinterpret_cast<const float2*>(sm + (iy * HM + ix) * 2);
+      const float2 v = srow[ky][x + kx];
       a = fmaf(w[ky * 7 + kx], v.x, a);
       a = fmaf(w[49 + ky * 7 + kx], v.y, a);
     }
@@ -410,28 +431,29 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
   const float cx = boxes[r * 4 + 0], cy = boxes[r * 4 + 1], bw = boxes[r * 4 + 2], bh = boxes[r * 4 + 3];
   {
     const float* hp = heat_out + (o + k) * HMP;
-    float m = -INFINITY, se = 0.f, sx = 0.f, sy = 0.f;
-    for (int i = lane; i < HMP; i += 64) {
-      const float h = hp[i];
-      if (h > m) {  // rescale running sums to the new max
-        const float c = expf(m - h);
-        se *= c; sx *= c; sy *= c;
-        m = h;
-      }
-      const float e = expf(h - m);
+    // all 49 values of the lane loaded at once, then a two-pass softmax:
+    // the wave max first, then the exp-weighted sums (butterfly-reduced)
+    constexpr int NV = HMP / 64;
+    static_assert(HMP % 64 == 0, "decode layout");
+    float v[NV];
+#pragma unroll
+    for (int t = 0; t < NV; ++t) v[t] = hp[lane + 64 * t];
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NV; ++t) m = fmaxf(m, v[t]);
+    m = wave_max(m);
+    float se = 0.f, sx = 0.f, sy = 0.f;
+#pragma unroll
+    for (int t = 0; t < NV; ++t) {
+      const int i = lane + 64 * t;
+      const float e = expf(v[t] - m);
       se += e;
       sx = fmaf(e, (float)(i % HM), sx);
       sy = fmaf(e, (float)(i / HM), sy);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const float m2 = __shfl_xor(m, off, 64);
-      const float se2 = __shfl_xor(se, off, 64), sx2 = __shfl_xor(sx, off, 64), sy2 = __shfl_xor(sy, off, 64);
-      const float mn = fmaxf(m, m2);
-      const float c1 = expf(m - mn), c2 = expf(m2 - mn);
-      se = se * c1 + se2 * c2; sx = sx * c1 + sx2 * c2; sy = sy * c1 + sy2 * c2;
-      m = mn;
-    }
+    se = wave_sum(se);
+    sx = wave_sum(sx);
+    sy = wave_sum(sy);
     if (lane == 0) {
       const float kx = (sx / se) / (float)(HM - 1);
       const float ky = (sy / se) / (float)(HM - 1);
