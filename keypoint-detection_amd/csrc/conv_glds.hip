@@ -909,6 +909,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = HP + (L / NTL) * BM, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
   const int Mtot = p.R * HPP, cin = p.cin, NC = cin / 64, KT = 9 * NC;
+  stamp16(p.stamps, 0);
   const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
@@ -1001,6 +1002,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     if (k < KT) issue_b(k);
   Half f0, f1;
   barrier_k(KT < SB - 1);
+  stamp16(p.stamps, 1);
   if (NC > 1) issue_a(1, 0);
   if (SB - 1 < KT) issue_b(SB - 1);
   load_half(0, 0, f0);
@@ -1021,11 +1023,14 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     } else {
       __builtin_amdgcn_s_waitcnt(0xC07F);
     }
+    // (threading the DMA pieces between the MFMA rows measured 2 % slower:
+    // the weights then land later than the next barrier wants them)
     __builtin_amdgcn_s_setprio(1);
     mma_half(f1);
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
+  stamp16(p.stamps, 2);
 
   // interior test of a padded position: ROI row/column 1..56
   auto interior = [&](int m, int& r, int& yy, int& xx) {
@@ -1121,6 +1126,11 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
         if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? kpd_sigmoid(val + fw[NKF * 64 + k]) : 0.f;
       }
     }
+  }
+  if (p.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp16(p.stamps, 3);
+    stamp16(p.stamps, 5, (unsigned long long)KT);
   }
 }
 

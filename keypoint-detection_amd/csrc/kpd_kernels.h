@@ -73,6 +73,7 @@ struct HmConvArgs {
   float* heat;
   int r0;                // first ROI of the launch chunk (launcher)
   int in_bytes, wt_bytes;   // launcher
+  unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_hmconv(const HmConvArgs& a, hipStream_t st);
 constexpr int kHmPad = 58;   // padded ROI side of the hmconv layout

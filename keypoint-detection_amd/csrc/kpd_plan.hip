@@ -640,12 +640,13 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
 // epilogue and write the heatmap instead of `out` (conv_glds.hip).
 struct HmFinal { const float *w, *b; const int32_t* slot; int P; float* heat; };
 int hm_conv(const kpd_plan* p, const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind,
-            hipStream_t st, const HmFinal* fin = nullptr) {
+            hipStream_t st, const HmFinal* fin = nullptr, unsigned long long* stamps = nullptr) {
   if (!L.bf16) return conv(L, in, R, 56, 56, in_cstride, out, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
   if (hm_padded(p)) {
     if (in_cstride != L.cin_p) return fail(KPD_EINVAL, "hmconv: input channel stride must equal cin");
     HmConvArgs h{};
     h.in = in; h.wt = L.w; h.bias = L.b; h.out = out; h.R = R; h.cin = L.cin_p; h.cout = L.cout_p;
+    h.stamps = stamps;
     if (fin) {
       if (out_kind != 2 || L.cout_p != 64) return fail(KPD_EINVAL, "fused final layer needs the 64-channel conv");
       h.fin_w = fin->w; h.fin_b = fin->b; h.slot = fin->slot; h.P = fin->P; h.heat = fin->heat;
@@ -960,6 +961,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     unsigned long long* r = p->stamps + stamp_off;
     stamp_off += wgs * 8;
     dbg[name] = {r, wgs * 64};
+    p->debug[name] = {r, wgs * 64};   // (p->debug is replaced by dbg mid-forward; heads register late)
     return r;
   };
 
@@ -1202,7 +1204,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st)) return rc;
   c1.reset();
   std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
-  if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st)) return rc;
+  if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st, nullptr,
+                       take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
+    return rc;
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
   // mixed: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)

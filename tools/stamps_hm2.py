@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Phase stamps of the heatmap conv 2 (hmconv_kernel, KPD_STAMPS): per
+workgroup the prologue (chunk 0 window + first weights landed), the K loop and
+the epilogue (stores drained).  GPU only:  KPD_STAMPS=1 python3 tools/stamps_hm2.py"""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "keypoint-detection_amd")]
+os.environ.setdefault("KPD_STAMPS", "1")
+
+
+def main():
+    from dll.configs import ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+    dev = torch.device("cuda:0")
+    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision="mixed", streams=1)
+    m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
+    m = m.to(dev).eval()
+    B = 64
+    batch = {"image": synthetic_images(B, 3, 256, 192, seed=1234).to(dev),
+             "bboxes": synthetic_boxes(B, 1, seed=1235).to(dev)}
+    plan = m.native_plan(dev)
+    with torch.no_grad():
+        for _ in range(4):
+            m(batch)
+    torch.cuda.synchronize()
+    st = plan.debug_buffer("stamps_hm2").view(torch.int64).cpu().numpy().reshape(-1, 8)
+    st = st[st[:, 0] != 0]
+    t = st[:, [0, 1, 2, 3]].astype(np.float64) * 0.01
+    t -= t[:, 0].min()
+    start, end = t[:, 0], t[:, 3]
+    ph = np.diff(t, axis=1)
+    print(f"wgs={len(st)} span={end.max():.1f}us KT={st[0, 5]} starts p10/p50/p90 {np.percentile(start, 10):.1f}/"
+          f"{np.median(start):.1f}/{np.percentile(start, 90):.1f}")
+    print("phases med (prologue, K loop, epilogue) = " + " ".join(f"{v:.2f}" for v in np.median(ph, axis=0))
+          + f"  K loop per step {np.median(ph[:, 1]) / st[0, 5]:.3f}us  wg med {np.median(end - start):.2f}")
+
+
+if __name__ == "__main__":
+    main()
