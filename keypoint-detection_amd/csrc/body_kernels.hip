@@ -847,20 +847,45 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
 
+  // a slice's weights are loaded into registers one slice ahead (issued
+  // before this slice's compute, stored to LDS after its barrier), so no
+  // slice waits on a global round trip for its weights.  (Padding the LDS
+  // pixel rows against bank conflicts with a one-pixel expand mapping
+  // measured 84 vs 51 us: more LDS reads per FMA; not kept.)
+  constexpr int PE = 4, PP = 4;   // cin_p * CS <= 1024, CS * cout_p <= 1024 (fir_pick_rows)
+  float pe[PE], pp[PP];
+  float4 pd = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto prefetch = [&](int c0) {
+#pragma unroll
+    for (int u = 0; u < PE; ++u) {
+      const int i = tid + u * 256, c = i / cin_p, k = i - c * cin_p;
+      pe[u] = i < cin_p * CS ? a.we[(size_t)(c0 + c) * cin_p + k] : 0.f;
+    }
+    if (tid < K * K * CQ) {
+      const int t = tid / CQ, q = tid - t * CQ;
+      pd = *reinterpret_cast<const float4*>(a.wd + (size_t)t * a.Ep + c0 + q * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int i = tid + u * 256, co = i / CS, c = i - co * CS;
+      pp[u] = i < CS * cout_p ? a.wp[(size_t)co * a.Ep + c0 + c] : 0.f;
+    }
+  };
+  prefetch(0);
   for (int c0 = 0; c0 < a.Ep; c0 += CS) {
     __syncthreads();   // previous slice's es / ds / weights fully consumed (and xs staged)
-    for (int i = tid; i < cin_p * CS; i += 256) {
-      const int c = i / cin_p, k = i - c * cin_p;
-      weT[k * CS + c] = a.we[(size_t)(c0 + c) * cin_p + k];
+#pragma unroll
+    for (int u = 0; u < PE; ++u) {
+      const int i = tid + u * 256, c = i / cin_p, k = i - c * cin_p;
+      if (i < cin_p * CS) weT[k * CS + c] = pe[u];
     }
-    for (int i = tid; i < K * K * CQ; i += 256) {
-      const int t = i / CQ, q = i - t * CQ;
-      reinterpret_cast<float4*>(wds)[i] = *reinterpret_cast<const float4*>(a.wd + (size_t)t * a.Ep + c0 + q * 4);
+    if (tid < K * K * CQ) reinterpret_cast<float4*>(wds)[tid] = pd;
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const int i = tid + u * 256, co = i / CS, c = i - co * CS;
+      if (i < CS * cout_p) wpT[c * cout_p + co] = pp[u];
     }
-    for (int i = tid; i < CS * cout_p; i += 256) {
-      const int co = i / CS, c = i - co * CS;
-      wpT[c * cout_p + co] = a.wp[(size_t)co * a.Ep + c0 + c];
-    }
+    if (c0 + CS < a.Ep) prefetch(c0 + CS);
     __syncthreads();
     // expand: 4 pixels x 4 channels per thread, weights from LDS
     const int pg_n = (npx_in + 3) / 4;
@@ -1263,7 +1288,9 @@ size_t fir_lds_bytes(const FirArgs& a, int K, int S) {
 }
 
 int fir_pick_rows(FirArgs& a, int K, int S) {
-  if (a.cin_p % 4 || a.Ep % FIR_CS || a.cout_p % 8 || (a.res && (S != 1 || a.cin_p != a.cout_p))) return 0;
+  if (a.cin_p % 4 || a.Ep % FIR_CS || a.cout_p % 8 || (a.res && (S != 1 || a.cin_p != a.cout_p)) ||
+      a.cin_p * FIR_CS > 1024 || FIR_CS * a.cout_p > 1024 || K * K * FIR_CS / 4 > 256)
+    return 0;
   static const int th_env = getenv("KPD_FIR_TH") ? atoi(getenv("KPD_FIR_TH")) : 0;   // A/B sweeps
   for (int th = std::min(a.Ho, th_env > 0 ? th_env : 16); th >= 1; --th) {
     a.TH = th;
