@@ -801,6 +801,94 @@ __global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict_
   for (int k = 0; k < 4; ++k) op[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
+// Small-K 1x1 conv (cin_p <= 96, cout_p % 64 == 0) + bias + act (+ nearest-
+// upsampled residual, + max|out|): the FPN laterals 1 / 2 (backbone.py:33-37,
+// top-down add) and features.12 (the last 96 -> 576 conv).  The generic
+// implicit-GEMM kernel stages through LDS and pays a K-loop prologue for a
+// single K-tile; here every operand goes straight from L2 to MFMA fragments
+// in one load round trip.  Workgroup = 64 pixels x 64 output channels; wave w
+// owns pixels 16w..16w+15 and all four 16-channel tiles.  fp32 operands on
+// v_mfma_f32_16x16x4_f32 (exact products), k-step t of a 16-wide chunk takes
+// element t of each lane's 16-byte load (same permutation for A and B).
+constexpr int kPwKC = 6;   // 16-wide k chunks (cin_p <= 96)
+__global__ __launch_bounds__(256) void pw_small_kernel(const ConvArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 64 + wave * 16, n0 = blockIdx.y * 64;
+  const int nkc = a.cin_p / 16, M = a.M;
+  const float* x = static_cast<const float*>(a.in);
+  const float* w = static_cast<const float*>(a.wt);
+  float4 av[kPwKC], bv[4][kPwKC];
+  const int pa = min(m0 + r, M - 1);
+#pragma unroll
+  for (int kc = 0; kc < kPwKC; ++kc)
+    av[kc] = kc < nkc ? *reinterpret_cast<const float4*>(x + (size_t)pa * a.in_cstride + kc * 16 + g * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int kc = 0; kc < kPwKC; ++kc)
+      bv[nt][kc] = kc < nkc ? *reinterpret_cast<const float4*>(w + (size_t)(n0 + nt * 16 + r) * a.cin_p + kc * 16 + g * 4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  // epilogue inputs issued before the MFMAs: bias, and the residual rows
+  float bias[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) bias[nt] = a.bias[n0 + nt * 16 + r];
+  const int HW = a.H * a.W;
+  float resv[4][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) resv[nt][i] = 0.f;
+  if (a.res) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = min(m0 + g * 4 + i, M - 1);
+      const int n = m / HW, rr = m - n * HW, y = rr / a.W, xx = rr - y * a.W;
+      int sy = y, sx = xx;
+      if (a.rh != a.H) sy = min((int)floorf((float)y * ((float)a.rh / (float)a.H)), a.rh - 1);
+      if (a.rw != a.W) sx = min((int)floorf((float)xx * ((float)a.rw / (float)a.W)), a.rw - 1);
+      const float* rp = a.res + ((size_t)(n * a.rh + sy) * a.rw + sx) * a.cout_p + n0 + r;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) resv[nt][i] = rp[nt * 16];
+    }
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kc = 0; kc < kPwKC; ++kc)
+    if (kc < nkc) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].x, bv[nt][kc].x, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].y, bv[nt][kc].y, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].z, bv[nt][kc].z, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kc].w, bv[nt][kc].w, acc[nt], 0, 0, 0);
+      }
+    }
+  // C layout: col = lane & 15 (channel), row = 4 * (lane >> 4) + i (pixel)
+  float* out = static_cast<float*>(a.out);
+  float m_abs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + g * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float v = kpd_act(acc[nt][i] + bias[nt], a.act) + resv[nt][i];
+      out[(size_t)m * a.out_cstride + n0 + nt * 16 + r] = v;
+      m_abs = fmaxf(m_abs, fabsf(v));
+    }
+  }
+  if (a.amax) {
+    __shared__ float red[4];
+    const float wm = wave_max(m_abs);
+    if (lane == 0) red[wave] = wm;
+    __syncthreads();
+    if (tid == 0) amax_publish(a.amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
 // Fused MobileNetV3 inverted residual without SE (features.2 / features.3 of
 // mobilenet_v3_small, backbone.py:250-254): expand 1x1 + act, depthwise KxK
 // stride S + act, project 1x1 (+ residual), on a tile of TH output rows x the
@@ -1414,6 +1502,23 @@ hipError_t launch_se16_proj(const float* d, int N, int npx, int ntiles, const fl
   if (sq > 16 || ntiles * 16 > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(se16_proj_kernel, dim3((npx + 255) / 256, N), dim3(256), 0, st, d, npx, ntiles, part, w1, b1, w2t,
                      b2, sq, wp, bp, out);
+  return hipGetLastError();
+}
+
+bool pw_small_ok(const ConvArgs& a) {
+  static const bool off = getenv("KPD_NO_PWSMALL") != nullptr;   // A/B switch
+  // large outputs keep the generic kernel's LDS-staged 16-byte stores: lateral
+  // 1 (6.3 M outputs at 64 images) measured 18.9 us here vs 17.6 us there;
+  // lateral 2 (1.6 M) 8.2 vs 17, the last conv (1.8 M) 12.9 vs 18
+  return !off && a.cin_p % 16 == 0 && a.cin_p <= 16 * kPwKC && a.cout_p % 64 == 0 && !a.a_scale && !a.stats &&
+         !a.post_scale && a.act3 == 0 && a.out_cstride >= a.cout_p && a.in_cstride % 4 == 0 && a.M > 0 &&
+         (long)a.M * a.cout_p <= (4L << 20);
+}
+
+hipError_t launch_pw_small(const ConvArgs& a, hipStream_t st) {
+  if (!pw_small_ok(a)) return hipErrorInvalidValue;
+  const dim3 grid((a.M + 63) / 64, a.cout_p / 64);
+  hipLaunchKernelGGL(pw_small_kernel, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -181,6 +181,10 @@ hipError_t launch_dwsum(const float* in, int N, int Hi, int Wi, const float* w, 
 hipError_t launch_se16_proj(const float* d, int N, int npx, int ntiles, const float* part, const float* w1,
                             const float* b1, const float* w2t, const float* b2, int sq, const float* wp,
                             const float* bp, float* out, hipStream_t st);
+// small-K fp32 1x1 conv with direct-to-fragment loads (body_kernels.hip,
+// pw_small_kernel): cin_p <= 96, cout_p % 64 == 0, act + optional residual/amax
+bool pw_small_ok(const ConvArgs& a);
+hipError_t launch_pw_small(const ConvArgs& a, hipStream_t st);
 // the excitation alone, for the wide blocks: sesc [N][Ep]
 hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,

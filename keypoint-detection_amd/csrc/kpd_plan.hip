@@ -629,6 +629,10 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
   a.rh = rh; a.rw = rw; a.act = act; a.M = N * H * W; a.tiles_per_img = tiles;
   a.splitk_ws = g_splitk; a.splitk_cap = kSplitKFloats;
   const ConvDType dt = !L.bf16 ? CONV_F32 : (out_kind == 1 ? CONV_BF16_OUT_BF16 : CONV_BF16_OUT_F32);
+  if (L.k == 1 && !L.bf16 && out_kind == 0 && pw_small_ok(a)) {   // small-K 1x1: direct-to-fragment MFMA
+    HIP_TRY(launch_pw_small(a, st));
+    return KPD_OK;
+  }
   HIP_TRY(launch_conv(a, dt, L.k, st));
   return KPD_OK;
 }
