@@ -544,6 +544,9 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 // (with an exact 4x upsample the taps outside the image are exactly the lat1
 // rows / columns outside the grid).  Register epilogue with the channel
 // statistics; rows past the image's class grid are masked out of them.
+// DBG (ablations, KPD_FPN0X_DBG; wrong results by design): 1 = no MFMA, 2 = no K-loop DMA,
+// 4 = output stores of one fragment only (the others go to an out-of-range offset)
+template <int DBG>
 __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int BN = 128, S = 3, WAVES_N = 2, WAVES_M = 4;
   constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
@@ -574,6 +577,10 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
 
   const i32x4 rf = make_rsrc(p.f_split, p.f_bytes), rl = make_rsrc(p.l_split, p.l_bytes);
   const i32x4 rw0 = make_rsrc(p.w0, p.w0_bytes), rwe = make_rsrc(p.weff, p.weff_bytes);
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, p.N * Hf * Wf * BN * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rst =
+      __builtin_amdgcn_make_buffer_rsrc(p.stats, (short)0, p.N * 16 * p.tpc * 2 * BN * 4, 0x00020000);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
   const unsigned a_dst = __builtin_amdgcn_readfirstlane(lds0 + wave * 32 * ROWB);
   const unsigned b_dst = __builtin_amdgcn_readfirstlane(lds0 + (BM + wave * (BN / 8)) * ROWB);
@@ -609,6 +616,36 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   int cls = 0, n = 0, jt = 0, ca = 0, cb = 0, q0 = 0, NG = 1, KT = 0, ld = 0;
   // masks packed: bits 0-8 = tap0 taps in the image, bits 9-12 = lat1 groups in the grid
   unsigned f_off[A_LD], l_off[A_LD], mask[A_LD];
+  const float inv_rw = 1.f / (float)rw;   // q / rw by a float product: exact for q < 2^16 (host check)
+  // Per-row offsets and masks of tile L (VALU only, no divides, one uniform
+  // LDS read of the class's group table).  Computed for the NEXT tile inside
+  // the K loop, where it overlaps the MFMAs, not between tiles where both
+  // waves of a SIMD would run it side by side (measured 3.6 us per tile).
+  auto rows = [&](int L, unsigned* fo, unsigned* lo, unsigned* mk) {
+    const int c = L & 15, nj = L >> 4, nn = nj / p.tpc, j = nj - nn * p.tpc;
+    const int a_ = c >> 2, b_ = c & 3, qb = j * BM, ng = s_ng[c];
+    const int4 gq = *reinterpret_cast<const int4*>(s_g + c * 4);
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int q = qb + wave * 32 + i * 8 + lrow;
+      const int Y = (int)(((float)q + 0.5f) * inv_rw), X = q - Y * rw, y = 4 * Y + a_, x = 4 * X + b_;
+      fo[i] = (unsigned)(((nn * Hf + y) * Wf + x) * 64);
+      lo[i] = (unsigned)(((nn * rh + Y) * rw + X) * 512);
+      // validity of rows / columns -1, 0, +1 around (y, x) and (Y, X) as 3-bit sets
+      const unsigned ry = (y > 0 ? 1u : 0u) | 2u | (y + 1 < Hf ? 4u : 0u);
+      const unsigned cx = (x > 0 ? 1u : 0u) | 2u | (x + 1 < Wf ? 4u : 0u);
+      const unsigned ryl = (Y > 0 ? 1u : 0u) | 2u | (Y + 1 < rh ? 4u : 0u);
+      const unsigned cxl = (X > 0 ? 1u : 0u) | 2u | (X + 1 < rw ? 4u : 0u);
+      unsigned m = (ry & 1u ? cx : 0u) | (ry & 2u ? cx << 3 : 0u) | (ry & 4u ? cx << 6 : 0u);
+      const int gg[4] = {gq.x, gq.y, gq.z, gq.w};
+#pragma unroll
+      for (int g = 0; g < kFpn0xMaxGroups; ++g) {
+        const int oy1 = (gg[g] * 11) >> 5, ox1 = gg[g] - 3 * oy1;   // gg / 3, gg % 3 for gg < 9
+        if (g < ng && ((ryl >> oy1) & (cxl >> ox1) & 1u)) m |= 1u << (9 + g);
+      }
+      mk[i] = q < RG ? m : 0u;
+    }
+  };
   auto setup = [&](int L) {
     cls = L & 15;
     const int nj = L >> 4;
@@ -620,28 +657,6 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     NG = s_ng[cls];
     KT = KT0 + 4 * NG;
     ld = 0;
-    // per staged row: tap0 pixel offset (64-byte rows) + 9-tap mask, lat1
-    // pixel offset (512-byte rows) + group mask
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      const int q = q0 + wave * 32 + i * 8 + lrow;
-      f_off[i] = l_off[i] = 0;
-      mask[i] = 0;
-      if (q < RG) {
-        const int Y = q / rw, X = q - Y * rw, y = 4 * Y + ca, x = 4 * X + cb;
-        f_off[i] = (unsigned)((((size_t)n * Hf + y) * Wf + x) * 64);
-        l_off[i] = (unsigned)((((size_t)n * rh + Y) * rw + X) * 512);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-          if (yy >= 0 && yy < Hf && xx >= 0 && xx < Wf) mask[i] |= 1u << t;
-        }
-        for (int g = 0; g < NG; ++g) {
-          const int gg = s_g[cls * 4 + g], oy = gg / 3 - 1, ox = gg % 3 - 1;
-          if (Y + oy >= 0 && Y + oy < rh && X + ox >= 0 && X + ox < rw) mask[i] |= 1u << (9 + g);
-        }
-      }
-    }
   };
   auto issue = [&](int stage) {
     const unsigned so = stage * STAGE;
@@ -698,6 +713,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(sb + b_row + j * 16 * ROWB + (hl ? ch1 : ch0));
   };
   auto pass = [&](const uint4* a, const uint4* b) {
+    if (DBG == 1) return;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -719,23 +735,37 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   int L = tile_at(0);
   if (L >= ntiles) return;
   setup(L);
+  rows(L, f_off, l_off, mask);
 #pragma unroll
   for (int s2 = 0; s2 < S - 1; ++s2)
     if (s2 < KT) issue(s2);
+  unsigned nf_off[A_LD], nl_off[A_LD], nmask[A_LD];   // the next tile's rows
   for (int round = 0; L < ntiles; ++round) {
+    const int Lnext = tile_at(round + 1);
     stamp16(p.stamps, 0, 0, L);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-      tile_ready(0);
+      if (round == 0) {
+        tile_ready(0);
+      } else {   // + the previous tile's FM*FN output and 1 stats stores, issued after this tile's prologue
+        wait_vmcnt<(S - 2) * LPT + FM * FN + 1>();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
       stamp16(p.stamps, 1, 0, L);
+      // Each K-tile is issued as soon as its stage is free: tile k+S-1 goes
+      // into the stage of tile k-1, whose fragments every wave has read into
+      // registers before barrier k.  Issuing right after that barrier (not at
+      // the top of the next iteration) gives each DMA ~2 iterations of lead
+      // instead of ~1.3; the loop is bound by the DMA latency x bytes in flight.
+      if (S - 1 < KT) issue(S - 1);
       rd_a(0, 1, fa1); rd_b(0, 0, fb0); rd_b(0, 1, fb1); rd_a(0, 0, fa0);
-      int is = S - 1, rs = 0;   // stage the next issue writes / stage of the current tile
+      int is = 0, rs = 0;   // stage the next issue writes / stage of the current tile
       for (int kt = 0; kt < KT; ++kt) {
-        if (kt + S - 1 < KT) issue(is);   // into the stage of tile kt-1 (free since barrier kt)
-        is = is + 1 == S ? 0 : is + 1;
         const int ns = rs + 1 == S ? 0 : rs + 1;
         const bool more = kt + 1 < KT;
         __builtin_amdgcn_s_setprio(1);
@@ -743,11 +773,14 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         __builtin_amdgcn_s_setprio(0);
         if (more) {
           tile_ready(kt + 1);
+          if (DBG != 2 && kt + S < KT) issue(is);   // tile kt+S into the stage of tile kt (read before barrier kt+1)
+          is = is + 1 == S ? 0 : is + 1;
           rd_a(ns, 1, fa1);
         }
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb1);
         __builtin_amdgcn_s_setprio(0);
+        if (kt == 0 && Lnext < ntiles) rows(Lnext, nf_off, nl_off, nmask);
         if (more) rd_b(ns, 1, fb1);
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb0);
@@ -764,17 +797,24 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     stamp16(p.stamps, 5, (unsigned long long)KT, L);
     // this tile's geometry for the epilogue; then the next tile's prologue
     const int e_cls = cls, e_n = n, e_jt = jt, e_ca = ca, e_cb = cb, e_q0 = q0;
-    const int Lnext = tile_at(round + 1);
     if (Lnext < ntiles) {
       setup(Lnext);
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        f_off[i] = nf_off[i];
+        l_off[i] = nl_off[i];
+        mask[i] = nmask[i];
+      }
 #pragma unroll
       for (int s2 = 0; s2 < S - 1; ++s2)
         if (s2 < KT) issue(s2);
     }
+    stamp16(p.stamps, 6, 0, L);
 
     // ---------------- register epilogue ----------------
     const int t4 = lane & 3, q4 = r16 >> 2;
     float* sts = reinterpret_cast<float*>(lds + RING);
+    const int row_lim = RG - (e_q0 + wm * WM + g * 4);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = wn * 64 + j * 16;
@@ -786,7 +826,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         for (int e = 0; e < 4; ++e) {
           const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
           acc[i][j][e] = v;
-          const bool row_ok = e_q0 + wm * WM + i * 16 + g * 4 + e < RG;
+          const bool row_ok = i * 16 + e < row_lim;
           sm += row_ok ? v : 0.f;
           mx = row_ok ? fmaxf(mx, v) : mx;
         }
@@ -802,16 +842,25 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (tid < BN) {
-      float sm = sts[tid], mx = sts[WAVES_M * BN + tid];
+    stamp16(p.stamps, 7, 0, L);
+    // Stats and output leave by buffer stores issued by EVERY wave in a fixed
+    // count (an out-of-range row goes to an out-of-range offset, dropped by
+    // the range check): the next tile's first tile_ready counts them (vmcnt
+    // retires loads, stores and LDS-DMA in issue order), so it waits for the
+    // next tile's first K-tile only, not for this tile's stores.
+    {
+      float v = 0.f;
+      if (tid < 2 * BN) {
+        const int c = tid & (BN - 1), mxs = tid >= BN;
+        v = sts[mxs * WAVES_M * BN + c];
 #pragma unroll
-      for (int w = 1; w < WAVES_M; ++w) {
-        sm += sts[w * BN + tid];
-        mx = fmaxf(mx, sts[(WAVES_M + w) * BN + tid]);
+        for (int w = 1; w < WAVES_M; ++w) {
+          const float u = sts[(mxs * WAVES_M + w) * BN + c];
+          v = mxs ? fmaxf(v, u) : v + u;
+        }
       }
-      float* st = p.stats + ((size_t)e_n * 16 * p.tpc + e_cls * p.tpc + e_jt) * 2 * BN;
-      st[tid] = sm;
-      st[BN + tid] = mx;
+      const unsigned so = (unsigned)(((e_n * 16 + e_cls) * p.tpc + e_jt) * 2 * BN) * 4u;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rst, tid < 2 * BN ? so + tid * 4 : OOB, 0, 0);
     }
     stamp16(p.stamps, 3, 0, L);
 #pragma unroll
@@ -821,12 +870,9 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         f32x4 v = acc[i][j];
         quad_transpose(v, t4);
         const int q = e_q0 + wm * WM + i * 16 + g * 4 + t4;
-        if (q < RG) {
-          const int Y = q / rw, X = q - Y * rw;
-          float* dst =
-              p.out + (((size_t)e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + j * 16 + q4 * 4;
-          *reinterpret_cast<f32x4*>(dst) = v;
-        }
+        const int Y = (int)(((float)q + 0.5f) * inv_rw), X = q - Y * rw;
+        const unsigned o = (unsigned)((((e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + j * 16 + q4 * 4) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, q < RG && (DBG != 4 || (i | j) == 0) ? o : OOB, 0, 0);
       }
     if (p.stamps) {   // diagnostic build path: the stores' completion
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1223,6 +1269,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   if (a.N <= 0) return hipSuccess;
   if (a.Hf != 4 * a.rh || a.Wf != 4 * a.rw || a.tpc != (a.rh * a.rw + BM - 1) / BM) return hipErrorInvalidValue;
+  if ((long)a.tpc * BM >= 65536) return hipErrorInvalidValue;   // the kernel's float q / rw
+  // 32-bit buffer offsets of the output and statistics stores
+  if ((long)a.N * a.Hf * a.Wf * 512 >= (1L << 31) || (long)a.N * 16 * a.tpc * 1024 >= (1L << 31))
+    return hipErrorInvalidValue;
   const long tiles = 16L * a.N * a.tpc;
   // persistent: one workgroup per CU (the kernel walks the tiles in rounds)
   static int ncu = 0;
@@ -1234,7 +1284,11 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   }
   static const int grid_env = getenv("KPD_FPN0X_GRID") ? atoi(getenv("KPD_FPN0X_GRID")) : 0;   // A/B
   const long grid = std::min<long>(tiles, grid_env > 0 ? grid_env : ncu);
-  hipLaunchKernelGGL(fpn0x_kernel, dim3((unsigned)grid), dim3(NT), 0, st, a);
+  static const int dbg = getenv("KPD_FPN0X_DBG") ? atoi(getenv("KPD_FPN0X_DBG")) : 0;   // ablations only
+  if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, a);
+  else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, a);
+  else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // raw buffer descriptor: base, stride 0, num_records = bytes (range-checked)
 __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {

@@ -33,16 +33,16 @@ def main():
     torch.cuda.synchronize()
     st = plan.debug_buffer("stamps_fpn0x").view(torch.int64).cpu().numpy().reshape(-1, 8)
     kt = st[:, 5]
-    t = st[:, [0, 1, 2, 3, 4]].astype(np.float64) * 0.01   # us
+    t = st[:, [0, 1, 2, 6, 7, 3, 4]].astype(np.float64) * 0.01   # us
     t -= t[:, 0].min()
-    start, end = t[:, 0], t[:, 4]
+    start, end = t[:, 0], t[:, 6]
     print(f"wgs={len(st)} span={end.max():.1f}us  starts p10/p50/p90 = {np.percentile(start, 10):.1f}/"
           f"{np.median(start):.1f}/{np.percentile(start, 90):.1f}")
     for k in sorted(set(kt.tolist())):
         sel = kt == k
         ph = np.diff(t[sel], axis=1)
         print(f"KT={k:2d} n={sel.sum():5d}  wg med={np.median(end[sel] - start[sel]):6.2f}us  phases med "
-              f"(prologue, K loop, stats, stores) = " + " ".join(f"{v:5.2f}" for v in np.median(ph, axis=0))
+              f"(prologue, K loop, next-tile setup+issue, epilogue math+exchange, stats store, stores) = " + " ".join(f"{v:5.2f}" for v in np.median(ph, axis=0))
               + f"  K-loop per tile {np.median(ph[:, 1]) / k:.3f}us")
     # concurrency
     ev = np.concatenate([np.stack([start, np.ones_like(start)], 1), np.stack([end, -np.ones_like(end)], 1)])
