@@ -545,7 +545,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 // rows / columns outside the grid).  Register epilogue with the channel
 // statistics; rows past the image's class grid are masked out of them.
 // DBG (ablations, KPD_FPN0X_DBG; wrong results by design): 1 = no MFMA, 2 = no K-loop DMA,
-// 4 = output stores of one fragment only (the others go to an out-of-range offset)
+// 4 = output stores of one piece only (the others go to an out-of-range offset)
 template <int DBG>
 __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int BN = 128, S = 3, WAVES_N = 2, WAVES_M = 4;
@@ -658,20 +658,25 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     KT = KT0 + 4 * NG;
     ld = 0;
   };
+  // tap0 K-tile k (taps 2k, 2k+1) of a tile with rows fo / mk (class-independent B)
+  auto issue_tap0 = [&](int stage, int k, const unsigned* fo, const unsigned* mk) {
+    const unsigned so = stage * STAGE;
+    const int t = 2 * k + f_tsel;
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const int delta = (dy * Wf + dx) * 64 + (int)f_byte;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const unsigned voff = (t < 9 && ((mk[i] >> t) & 1u)) ? fo[i] + delta : OOB;
+      glds16(rf, a_dst + so + i * 8 * ROWB, voff, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i)
+      glds16(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + k) * ROWB + lchunk * 16), 0);
+  };
   auto issue = [&](int stage) {
     const unsigned so = stage * STAGE;
     if (ld < KT0) {
-      const int t = 2 * ld + f_tsel;
-      const int dy = t / 3 - 1, dx = t % 3 - 1;
-      const int delta = (dy * Wf + dx) * 64 + (int)f_byte;
-#pragma unroll
-      for (int i = 0; i < A_LD; ++i) {
-        const unsigned voff = (t < 9 && ((mask[i] >> t) & 1u)) ? f_off[i] + delta : OOB;
-        glds16(rf, a_dst + so + i * 8 * ROWB, voff, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < B_LD; ++i)
-        glds16(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + ld) * ROWB + lchunk * 16), 0);
+      issue_tap0(stage, ld, f_off, mask);
     } else {
       const int k = ld - KT0, g = k >> 2, kc = k & 3;
       const int gg = s_g[cls * 4 + g], oy = gg / 3 - 1, ox = gg % 3 - 1;
@@ -721,50 +726,55 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, b[j]),
                                                            acc[i][j], 0, 0, 0);
   };
-  // the DMAs of K-tile k landed: every DMA younger than it belongs to the
-  // (S-2) later K-tiles, or is a store of the previous tile's epilogue
-  // (stores are counted in vmcnt too: they can only make this wait longer)
-  auto tile_ready = [&](int k) {
-    if (k + S - 2 < KT) wait_vmcnt<(S - 2) * LPT>();
-    else wait_vmcnt<0>();
+  auto barrier_lds = [&]() {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+  };
+  // The DMAs of K-tile k (k >= 1) landed.  vmcnt retires in issue order; the
+  // ops younger than tile k are: the next K-tile (tile k+1, or the next
+  // tile's K-tile 0 when k is the last), and for k = 1, 2 of a round > 0
+  // the previous tile's FM*FN + 1 epilogue stores (issued after this tile's
+  // K-tile 2, which the previous round prefetched).
+  constexpr int NST = FM * FN + 1;
+  auto tile_ready = [&](int k, bool younger, bool after_stores) {
+    if (!younger) wait_vmcnt<0>();
+    else if (after_stores) wait_vmcnt<LPT + NST>();
+    else wait_vmcnt<LPT>();
+    barrier_lds();
   };
 
   int L = tile_at(0);
   if (L >= ntiles) return;
   setup(L);
   rows(L, f_off, l_off, mask);
+  static_assert(KT0 >= S, "the prefetched K-tiles of the next tile are tap0 K-tiles");
+  // Every round starts with its first S K-tiles issued: round 0 here, later
+  // rounds by the previous round (two inside its K loop, one after it).
 #pragma unroll
-  for (int s2 = 0; s2 < S - 1; ++s2)
-    if (s2 < KT) issue(s2);
+  for (int s2 = 0; s2 < S; ++s2) issue(s2);
   unsigned nf_off[A_LD], nl_off[A_LD], nmask[A_LD];   // the next tile's rows
+  int sb = 0;                                          // ring stage of this tile's K-tile 0
   for (int round = 0; L < ntiles; ++round) {
     const int Lnext = tile_at(round + 1);
+    const bool has_next = Lnext < ntiles;
     stamp16(p.stamps, 0, 0, L);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-      if (round == 0) {
-        tile_ready(0);
-      } else {   // + the previous tile's FM*FN output and 1 stats stores, issued after this tile's prologue
-        wait_vmcnt<(S - 2) * LPT + FM * FN + 1>();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
+      // K-tile 0 landed: younger are K-tiles 1, 2 (and in a round > 0 the
+      // previous tile's stores)
+      if (round == 0) wait_vmcnt<(S - 1) * LPT>();
+      else wait_vmcnt<(S - 1) * LPT + NST>();
+      barrier_lds();
       stamp16(p.stamps, 1, 0, L);
-      // Each K-tile is issued as soon as its stage is free: tile k+S-1 goes
-      // into the stage of tile k-1, whose fragments every wave has read into
-      // registers before barrier k.  Issuing right after that barrier (not at
-      // the top of the next iteration) gives each DMA ~2 iterations of lead
-      // instead of ~1.3; the loop is bound by the DMA latency x bytes in flight.
-      if (S - 1 < KT) issue(S - 1);
-      rd_a(0, 1, fa1); rd_b(0, 0, fb0); rd_b(0, 1, fb1); rd_a(0, 0, fa0);
-      int is = 0, rs = 0;   // stage the next issue writes / stage of the current tile
+      rd_a(sb, 1, fa1); rd_b(sb, 0, fb0); rd_b(sb, 1, fb1); rd_a(sb, 0, fa0);
+      // Each K-tile is issued as soon as its stage is free: after barrier
+      // kt+1 every wave has read tile kt into registers, so tile kt+S (or,
+      // near the end, the next tile's K-tile kt+S-KT) goes into its stage.
+      int is = sb, rs = sb;   // stage the next issue writes / stage of the current tile
       for (int kt = 0; kt < KT; ++kt) {
         const int ns = rs + 1 == S ? 0 : rs + 1;
         const bool more = kt + 1 < KT;
@@ -772,15 +782,18 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         pass(fa1, fb0);
         __builtin_amdgcn_s_setprio(0);
         if (more) {
-          tile_ready(kt + 1);
-          if (DBG != 2 && kt + S < KT) issue(is);   // tile kt+S into the stage of tile kt (read before barrier kt+1)
+          tile_ready(kt + 1, kt + 2 < KT || has_next, round > 0 && kt + 1 <= 2);
+          if (DBG != 2) {
+            if (kt + S < KT) issue(is);
+            else if (has_next) issue_tap0(is, kt + S - KT, nf_off, nmask);
+          }
           is = is + 1 == S ? 0 : is + 1;
           rd_a(ns, 1, fa1);
         }
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb1);
         __builtin_amdgcn_s_setprio(0);
-        if (kt == 0 && Lnext < ntiles) rows(Lnext, nf_off, nl_off, nmask);
+        if (kt == 0 && has_next) rows(Lnext, nf_off, nl_off, nmask);
         if (more) rd_b(ns, 1, fb1);
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb0);
@@ -792,12 +805,14 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         rs = ns;
       }
     }
-    __syncthreads();   // every wave's fragment reads of the ring retired: the ring is free
+    barrier_lds();   // every wave's fragment reads of the ring retired: the stage of the last K-tile is free
     stamp16(p.stamps, 2, 0, L);
     stamp16(p.stamps, 5, (unsigned long long)KT, L);
     // this tile's geometry for the epilogue; then the next tile's prologue
     const int e_cls = cls, e_n = n, e_jt = jt, e_ca = ca, e_cb = cb, e_q0 = q0;
-    if (Lnext < ntiles) {
+    if (has_next) {
+      const int last = sb + KT - 1;   // the stage of this tile's last K-tile
+      sb = (sb + KT) % S;
       setup(Lnext);
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
@@ -805,9 +820,9 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         l_off[i] = nl_off[i];
         mask[i] = nmask[i];
       }
-#pragma unroll
-      for (int s2 = 0; s2 < S - 1; ++s2)
-        if (s2 < KT) issue(s2);
+      ld = S - 1;
+      if (DBG != 2) issue(last % S);   // the next tile's K-tile S-1 (0 .. S-2 went out inside the K loop)
+      else ++ld;
     }
     stamp16(p.stamps, 6, 0, L);
 
@@ -863,16 +878,28 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rst, tid < 2 * BN ? so + tid * 4 : OOB, 0, 0);
     }
     stamp16(p.stamps, 3, 0, L);
+    // Output pieces of 4 pixels x 64 channels (256 contiguous bytes per
+    // pixel, whole 128-byte lines): piece (i, e) gathers acc[i][0..3][e]
+    // (lane (g, r16): channels r16 + 16 j of pixel 16 i + 4 g + e), a quad
+    // transpose and a lane transpose inside each 16-lane row (lane 4p+q <-
+    // 4q+p, ds_bpermute) leave lane (g, c) with channels 4c .. 4c+3.  The
+    // 64-byte pieces of the plain fragment layout took ~35 us more per launch.
+    const int src4 = ((lane & 0x30) | ((lane & 3) << 2) | ((lane >> 2) & 3)) * 4;
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        f32x4 v = acc[i][j];
+      for (int e = 0; e < 4; ++e) {
+        f32x4 v = f32x4{acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
         quad_transpose(v, t4);
-        const int q = e_q0 + wm * WM + i * 16 + g * 4 + t4;
+        f32x4 w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = __int_as_float(__builtin_amdgcn_ds_bpermute(src4, __float_as_int(v[k])));
+        const int q = e_q0 + wm * WM + i * 16 + g * 4 + e;
         const int Y = (int)(((float)q + 0.5f) * inv_rw), X = q - Y * rw;
-        const unsigned o = (unsigned)((((e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + j * 16 + q4 * 4) * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rout, q < RG && (DBG != 4 || (i | j) == 0) ? o : OOB, 0, 0);
+        const unsigned o =
+            (unsigned)((((e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + r16 * 4) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout,
+                                               q < RG && (DBG != 4 || (i | e) == 0) ? o : OOB, 0, 0);
       }
     if (p.stamps) {   // diagnostic build path: the stores' completion
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
