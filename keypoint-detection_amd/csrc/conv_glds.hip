@@ -830,21 +830,36 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     const int t4 = lane & 3, q4 = r16 >> 2;
     float* sts = reinterpret_cast<float*>(lds + RING);
     const int row_lim = RG - (e_q0 + wm * WM + g * 4);
+    const bool full = e_q0 + BM <= RG;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = wn * 64 + j * 16;
       const float bj = s_bias[col + r16];
       float sm = 0.f, mx = -INFINITY;
+      if (full) {   // every row of the tile is in the grid: no masks, max3 pairs
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
-          acc[i][j][e] = v;
-          const bool row_ok = i * 16 + e < row_lim;
-          sm += row_ok ? v : 0.f;
-          mx = row_ok ? fmaxf(mx, v) : mx;
-        }
+          for (int e = 0; e < 4; e += 2) {
+            const float v0 = fmaxf(acc[i][j][e] * scale + bj, 0.f), v1 = fmaxf(acc[i][j][e + 1] * scale + bj, 0.f);
+            acc[i][j][e] = v0;
+            acc[i][j][e + 1] = v1;
+            sm += v0;
+            sm += v1;
+            mx = fmaxf(mx, fmaxf(v0, v1));
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
+            acc[i][j][e] = v;
+            const bool row_ok = i * 16 + e < row_lim;
+            sm += row_ok ? v : 0.f;
+            mx = row_ok ? fmaxf(mx, v) : mx;
+          }
+      }
       sm += __shfl_xor(sm, 16);
       mx = fmaxf(mx, __shfl_xor(mx, 16));
       sm += __shfl_xor(sm, 32);
