@@ -36,56 +36,73 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
                                                    const float* __restrict__ w, const float* __restrict__ b,
                                                    float* __restrict__ out, int Ho, int Wo,
                                                    float* __restrict__ amax) {
-  constexpr int Cin = CIN;
-  __shared__ float4 so[256 * 4];
-  __shared__ float sw[16 * 27];
-  __shared__ float sb[16];
+  constexpr int Cin = CIN, PT = 2;   // PT output pixels per thread: pix0 + t and pix0 + 256 + t
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  __shared__ float4 so[256 * PT * 4];
   __shared__ float red[4];
-  const int nw = 16 * Cin * 9;
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = w[i];
-  if (threadIdx.x < 16) sb[threadIdx.x] = b[threadIdx.x];
-  __syncthreads();
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = pix < N * Ho * Wo;
-  const int n = pix / (Ho * Wo), r = pix - n * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
-  float in[Cin * 9];
+  const int t = threadIdx.x, total = N * Ho * Wo;
+  const int pix0 = blockIdx.x * 256 * PT;
+  // all 9*CIN loads of both pixels issued unconditionally (clamped address,
+  // zero selected afterwards): no exec-mask branch per tap
+  f2 in[Cin * 9];
+  bool live[PT];
 #pragma unroll
-  for (int c = 0; c < Cin; ++c)
+  for (int u = 0; u < PT; ++u) {
+    const int pix = pix0 + u * 256 + t;
+    live[u] = pix < total;
+    const int pc = live[u] ? pix : 0;
+    const int n = pc / (Ho * Wo), r = pc - n * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
+    const float* ib = img + (size_t)n * Cin * H * W;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int c = 0; c < Cin; ++c)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iy = oy * 2 - 1 + ky, ix = ox * 2 - 1 + kx;
-        in[c * 9 + ky * 3 + kx] = (live && iy >= 0 && iy < H && ix >= 0 && ix < W)
-                                      ? img[((size_t)(n * Cin + c) * H + iy) * W + ix] : 0.f;
-      }
-  float o[16];
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int iy = oy * 2 - 1 + ky, ix = ox * 2 - 1 + kx;
+          const bool ok = live[u] && iy >= 0 && iy < H && ix >= 0 && ix < W;
+          const float v = ib[((size_t)c * H + min(max(iy, 0), H - 1)) * W + min(max(ix, 0), W - 1)];
+          in[c * 9 + ky * 3 + kx][u] = ok ? v : 0.f;
+        }
+  }
+  // weights and bias at wave-uniform addresses (scalar loads); the two pixels
+  // share each weight in one packed FMA
+  f2 o[16];
   float m_abs = 0.f;
 #pragma unroll
   for (int co = 0; co < 16; ++co) {
-    float a = 0.f;
+    f2 a = f2{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < Cin * 9; ++k) a = fmaf(in[k], sw[co * Cin * 9 + k], a);
-    o[co] = kpd_act(a + sb[co], ACT_HSWISH);
-    m_abs = fmaxf(m_abs, fabsf(o[co]));
+    for (int k = 0; k < Cin * 9; ++k) {
+      const float wk = w[co * Cin * 9 + k];
+      a = __builtin_elementwise_fma(in[k], f2{wk, wk}, a);
+    }
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      o[co][u] = kpd_act(a[u] + b[co], ACT_HSWISH);
+      if (live[u]) m_abs = fmaxf(m_abs, fabsf(o[co][u]));
+    }
   }
-  // stage the block's 256 x 64-byte outputs in LDS (XOR-swizzled quads), then
-  // store them as one contiguous 16 KB run: each store instruction covers
+  // stage the block's 512 x 64-byte outputs in LDS (XOR-swizzled quads), then
+  // store them as one contiguous 32 KB run: each store instruction covers
   // 1 KB of consecutive addresses instead of a 16-byte piece of every 64
-  const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    so[t * 4 + (q ^ (t & 3))] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  for (int u = 0; u < PT; ++u) {
+    const int lp = u * 256 + t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      so[lp * 4 + (q ^ (lp & 3))] = make_float4(o[4 * q][u], o[4 * q + 1][u], o[4 * q + 2][u], o[4 * q + 3][u]);
+  }
   __syncthreads();
-  const int pix0 = blockIdx.x * blockDim.x, npx = min(256, N * Ho * Wo - pix0);
+  const int npx = min(256 * PT, total - pix0);
   float4* dst = reinterpret_cast<float4*>(out + (size_t)pix0 * 16);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 4 * PT; ++q) {
     const int i = q * 256 + t, px = i >> 2, qq = i & 3;
     if (px < npx) dst[i] = so[px * 4 + (qq ^ (px & 3))];
   }
   if (amax) {   // max|tap0| for the split FPN scale bound (conv_glds.hip)
-    const float wm = wave_max(live ? m_abs : 0.f);
+    const float wm = wave_max(m_abs);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1311,10 +1328,10 @@ hipError_t launch_stem(const float* img, int N, int Cin, int H, int W, const flo
                        float* out, int Ho, int Wo, float* amax, hipStream_t st) {
   const int total = N * Ho * Wo;
   if (Cin == 3)
-    hipLaunchKernelGGL(stem_kernel<3>, dim3((total + 255) / 256), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
+    hipLaunchKernelGGL(stem_kernel<3>, dim3((total + 511) / 512), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
                        Wo, amax);
   else if (Cin == 1)
-    hipLaunchKernelGGL(stem_kernel<1>, dim3((total + 255) / 256), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
+    hipLaunchKernelGGL(stem_kernel<1>, dim3((total + 511) / 512), dim3(256), 0, st, img, N, H, W, w, b, out, Ho,
                        Wo, amax);
   else
     return hipErrorInvalidValue;

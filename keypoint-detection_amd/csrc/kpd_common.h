@@ -8,6 +8,15 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
+// x / 6 without the IEEE division sequence (v_div_scale / fmas / fixup, ~10
+// instructions): quotient by the rounded reciprocal, then one exact-residual
+// correction, which returns the correctly rounded quotient.
+__device__ __forceinline__ float kpd_div6(float x) {
+  constexpr float r6 = 1.f / 6.f;
+  const float q = x * r6;
+  return fmaf(fmaf(-q, 6.f, x), r6, q);
+}
+
 enum KpdAct : int { ACT_NONE = 0, ACT_RELU = 1, ACT_RELU6 = 2, ACT_HSWISH = 3, ACT_SIGMOID = 4 };
 
 // Activation formulas follow ATen's CPU kernels operation-for-operation
@@ -16,14 +25,14 @@ __device__ __forceinline__ float kpd_act(float v, int act) {
   switch (act) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_RELU6: return fminf(fmaxf(v, 0.f), 6.f);
-    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
+    case ACT_HSWISH: return kpd_div6(v * fminf(fmaxf(v + 3.f, 0.f), 6.f));
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
   }
 }
 
 __device__ __forceinline__ float kpd_sigmoid(float v) { return 1.f / (1.f + expf(-v)); }
-__device__ __forceinline__ float kpd_hsigmoid(float v) { return fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f; }
+__device__ __forceinline__ float kpd_hsigmoid(float v) { return kpd_div6(fminf(fmaxf(v + 3.f, 0.f), 6.f)); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
