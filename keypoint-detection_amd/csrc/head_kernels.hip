@@ -18,6 +18,7 @@
 
 namespace {
 constexpr int HM = 56;              // ROI / heatmap side
+static_assert(HM % 4 == 0, "hm_spool / hm_sapply take 4 pixels per load instruction");
 constexpr int HMP = HM * HM;        // 3136
 constexpr int NK = 17;              // keypoints
 constexpr int TOPK = 64;
@@ -266,43 +267,65 @@ __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__
   cw[(size_t)r * TOPK + c] = kpd_sigmoid(oa + om);
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 // ---------------------------------------------------------------- spatial pool
-// grid (56 rows, R), 64 threads (one output pixel x each; 56 active).
-// smap[r][y][x] = {mean_c, max_c} of roi*cw.
+// grid (56 rows, R), one wave.  smap[r][y][x] = {mean_c, max_c} of roi*cw.
+// Lane (p, c) = (lane >> 4, lane & 15) holds channels 4c .. 4c+3 of pixel
+// 4i + p: every load instruction reads 4 whole 256-byte pixel rows (1 KiB
+// contiguous; a pixel per lane touched 64 lines per instruction), and all 14
+// loads of the row are in flight before the first use.  The channel sum runs
+// 4-wide in the lane, then over the 16 lanes of the pixel (xor 1, 2, 4, 8).
 __global__ __launch_bounds__(64) void hm_spool_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
                                                       float* __restrict__ smap) {
-  __shared__ float scw[TOPK];
-  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
-  scw[x] = cw[(size_t)r * TOPK + x];
-  __syncthreads();
-  if (x >= HM) return;
-  const size_t pix = ((size_t)r * HM + y) * HM + x;
-  const float4* src = reinterpret_cast<const float4*>(roi + pix * TOPK);
-  float s = 0.f, m = -INFINITY;
+  constexpr int NI = HM / 4;
+  const int y = blockIdx.x, r = blockIdx.y, lane = threadIdx.x, pp = lane >> 4, c = lane & 15;
+  const float4* src = reinterpret_cast<const float4*>(roi + ((size_t)r * HM + y) * HM * TOPK);
+  float4 v[NI];
 #pragma unroll
-  for (int q = 0; q < TOPK / 4; ++q) {
-    const float4 v = src[q];
-    const float a = v.x * scw[4 * q], b = v.y * scw[4 * q + 1], c = v.z * scw[4 * q + 2], d = v.w * scw[4 * q + 3];
-    s += a; s += b; s += c; s += d;
-    m = fmaxf(fmaxf(m, a), fmaxf(b, fmaxf(c, d)));
+  for (int i = 0; i < NI; ++i) v[i] = src[(4 * i + pp) * (TOPK / 4) + c];
+  const float4 w = reinterpret_cast<const float4*>(cw + (size_t)r * TOPK)[c];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const float a = v[i].x * w.x, b = v[i].y * w.y, cc = v[i].z * w.z, d = v[i].w * w.w;
+    float s = (a + b) + (cc + d), m = fmaxf(fmaxf(a, b), fmaxf(cc, d));
+    // all-reduce inside the 16-lane row by DPP (quad xor 1, 2; row rotate 4, 8)
+    s += dpp_f<0xB1>(s); m = fmaxf(m, dpp_f<0xB1>(m));
+    s += dpp_f<0x4E>(s); m = fmaxf(m, dpp_f<0x4E>(m));
+    s += dpp_f<0x124>(s); m = fmaxf(m, dpp_f<0x124>(m));
+    s += dpp_f<0x128>(s); m = fmaxf(m, dpp_f<0x128>(m));
+    if (c == 0) {
+      const size_t pix = ((size_t)r * HM + y) * HM + 4 * i + pp;
+      *reinterpret_cast<float2*>(smap + pix * 2) = make_float2(s / (float)TOPK, m);
+    }
   }
-  smap[pix * 2 + 0] = s / (float)TOPK;
-  smap[pix * 2 + 1] = m;
 }
 
 // ---------------------------------------------------------------- spatial apply
-// grid (56 rows, R), 64 threads.  sw = sigmoid(conv7x7([mean,max]) + b);
-// xs = (roi * cw) * sw stored as the first heatmap conv's operand (bf16 or f32).
+// grid (56 rows, R), one wave.  sw = sigmoid(conv7x7([mean,max]) + b) per
+// pixel (lane x < 56, LDS), then xs = (roi * cw) * sw with lane (p, c) on
+// channels 4c .. 4c+3 of pixel 4i + p (1 KiB contiguous per load, the roi row
+// loads issued first), stored as the first heatmap conv's operand: bf16
+// zero-bordered [R][58][58][64] (out_bf16 == 2), bf16 [R][3136][64] (1) or
+// f32 (0).
 __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
                                                        const float* __restrict__ smap, const float* __restrict__ saw,
                                                        const float* __restrict__ sab, void* __restrict__ xs,
                                                        int out_bf16) {
-  __shared__ float scw[TOPK];
+  constexpr int NI = HM / 4;
   __shared__ float w[98];
   __shared__ float2 srow[7][HM + 6];   // the 7 smap rows around y, zero-padded by 3 columns
-  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x;
+  __shared__ float ssw[HM];
+  const int y = blockIdx.x, r = blockIdx.y, x = threadIdx.x, pp = x >> 4, c = x & 15;
   const float* sm = smap + (size_t)r * HMP * 2;
+  const float4* src = reinterpret_cast<const float4*>(roi + ((size_t)r * HM + y) * HM * TOPK);
+  float4 v[NI];
   {   // every load of the workgroup issued before the first LDS store
+#pragma unroll
+    for (int i = 0; i < NI; ++i) v[i] = src[(4 * i + pp) * (TOPK / 4) + c];
     float2 sv[7];
 #pragma unroll
     for (int ky = 0; ky < 7; ++ky) {
@@ -310,58 +333,49 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
       sv[ky] = (x < HM && iy >= 0 && iy < HM) ? *reinterpret_cast<const float2*>(sm + (iy * HM + x) * 2)
                                                 : make_float2(0.f, 0.f);
     }
-    const float cwv = cw[(size_t)r * TOPK + x];
     const float w0v = saw[x], w1v = x + 64 < 98 ? saw[x + 64] : 0.f;
 #pragma unroll
     for (int ky = 0; ky < 7; ++ky) {
       if (x < HM) srow[ky][x + 3] = sv[ky];
       if (x < 3) { srow[ky][x] = make_float2(0.f, 0.f); srow[ky][HM + 3 + x] = make_float2(0.f, 0.f); }
     }
-    scw[x] = cwv;
     w[x] = w0v;
     if (x + 64 < 98) w[x + 64] = w1v;
   }
   __syncthreads();
-  if (x >= HM) return;
-  // same tap order (ky, kx) as the reference conv; out-of-image taps add 0
-  float a = 0.f;
+  if (x < HM) {
+    // same tap order (ky, kx) as the reference conv; out-of-image taps add 0
+    float a = 0.f;
 #pragma unroll
-  for (int ky = 0; ky < 7; ++ky) {
-    const int iy = y + ky - 3;
-    if (iy < 0 || iy >= HM) continue;
+    for (int ky = 0; ky < 7; ++ky) {
+      const int iy = y + ky - 3;
+      if (iy < 0 || iy >= HM) continue;
 #pragma unroll
-    for (int kx = 0; kx < 7; ++kx) {
-      const int ix = x + kx - 3;
-      if (ix < 0 || ix >= HM) continue;
-      const float2 v = srow[ky][x + kx];
-      a = fmaf(w[ky * 7 + kx], v.x, a);
-      a = fmaf(w[49 + ky * 7 + kx], v.y, a);
+      for (int kx = 0; kx < 7; ++kx) {
+        const int ix = x + kx - 3;
+        if (ix < 0 || ix >= HM) continue;
+        const float2 sv2 = srow[ky][x + kx];
+        a = fmaf(w[ky * 7 + kx], sv2.x, a);
+        a = fmaf(w[49 + ky * 7 + kx], sv2.y, a);
+      }
     }
+    ssw[x] = kpd_sigmoid(a + sab[0]);
   }
-  const float sw = kpd_sigmoid(a + sab[0]);
-  const size_t pix = ((size_t)r * HM + y) * HM + x;
-  const float4* src = reinterpret_cast<const float4*>(roi + pix * TOPK);
-  if (out_bf16) {
-    // out_bf16 == 2: the zero-bordered [R][58][58][64] layout of hmconv_kernel
-    const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + x + 1 : pix;
-    __bf16* dst = reinterpret_cast<__bf16*>(xs) + opix * TOPK;
+  const float4 cq = reinterpret_cast<const float4*>(cw + (size_t)r * TOPK)[c];
+  __syncthreads();
 #pragma unroll
-    for (int q = 0; q < TOPK / 8; ++q) {
-      const float4 u = src[2 * q], v = src[2 * q + 1];
-      bf16x8 o;
-      o[0] = (__bf16)((u.x * scw[8 * q + 0]) * sw); o[1] = (__bf16)((u.y * scw[8 * q + 1]) * sw);
-      o[2] = (__bf16)((u.z * scw[8 * q + 2]) * sw); o[3] = (__bf16)((u.w * scw[8 * q + 3]) * sw);
-      o[4] = (__bf16)((v.x * scw[8 * q + 4]) * sw); o[5] = (__bf16)((v.y * scw[8 * q + 5]) * sw);
-      o[6] = (__bf16)((v.z * scw[8 * q + 6]) * sw); o[7] = (__bf16)((v.w * scw[8 * q + 7]) * sw);
-      *reinterpret_cast<bf16x8*>(dst + 8 * q) = o;
-    }
-  } else {
-    float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(xs) + pix * TOPK);
-#pragma unroll
-    for (int q = 0; q < TOPK / 4; ++q) {
-      const float4 u = src[q];
-      dst[q] = make_float4((u.x * scw[4 * q]) * sw, (u.y * scw[4 * q + 1]) * sw, (u.z * scw[4 * q + 2]) * sw,
-                           (u.w * scw[4 * q + 3]) * sw);
+  for (int i = 0; i < NI; ++i) {
+    const int px = 4 * i + pp;
+    const float sw = ssw[px];
+    const float4 o = make_float4((v[i].x * cq.x) * sw, (v[i].y * cq.y) * sw, (v[i].z * cq.z) * sw, (v[i].w * cq.w) * sw);
+    if (out_bf16) {
+      const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1
+                                        : ((size_t)r * HM + y) * HM + px;
+      bf16x4 ob;
+      ob[0] = (__bf16)o.x; ob[1] = (__bf16)o.y; ob[2] = (__bf16)o.z; ob[3] = (__bf16)o.w;
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(xs) + opix * TOPK + 4 * c) = ob;
+    } else {
+      reinterpret_cast<float4*>(reinterpret_cast<float*>(xs) + (((size_t)r * HM + y) * HM + px) * TOPK)[c] = o;
     }
   }
 }
