@@ -977,16 +977,19 @@ constexpr int HP = 58, HPP = HP * HP;   // padded ROI side, positions per ROI
 constexpr int AWIN = 384;               // A window rows per chunk
 // DBG (A/B ablations, KPD_HMCONV_DBG): 1 = no MFMA, 2 = no weight / window
 // DMA inside the K loop (the prologue's still lands)
-template <int BN, int SB, int DBG = 0>
+// BMH: GEMM rows per tile (256, or 224 so that the tile count packs the CUs'
+// rounds better -- launch_hmconv picks it; the window stays 384 rows)
+template <int BN, int SB, int DBG = 0, int BMH = BM>
 __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
-  constexpr int WM = BM / WAVES_M, FM = WM / 16, FN = 4;
+  constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
+  static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
   constexpr int A_LD = AWIN / 8 / 8;                     // A-window DMA wave-instructions per wave (6)
   constexpr int B_LD = BN / 64;                          // B DMA wave-instructions per wave per K-step
   constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB;
   constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
   constexpr bool FINAL = BN == 64;
-  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BM, 128, NT>();
+  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BMH, 128, NT>();
   constexpr int LDS = RING > EPI ? RING : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -995,7 +998,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int NTL = p.cout / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = HP + (L / NTL) * BM, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
+  const int m0 = HP + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
   const int Mtot = p.R * HPP, cin = p.cin, NC = cin / 64, KT = 9 * NC;
   stamp16(p.stamps, 0);
   const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
@@ -1131,7 +1134,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   if constexpr (!FINAL) {
     // bias + ReLU, bf16, 16-byte row stores through the LDS tile (two 128-column halves)
     float* tile = reinterpret_cast<float*>(lds);
-    constexpr int P4 = 128 + 4, C4 = 32, RS = NT / C4, IT = BM / RS;
+    constexpr int P4 = 128 + 4, C4 = 32, RS = NT / C4, IT = BMH / RS;
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
 #pragma unroll
     for (int h = 0; h < BN / 128; ++h) {
@@ -1295,9 +1298,23 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // stages for conv 1 / 2 (89 / 233 us vs 92 / 256 us at 64 ROIs): the
     // wider tile halves the weight bytes per MFMA; conv 3 has 64 outputs
     const int bn = fin ? 64 : (a.cout % 256 == 0 ? 256 : 128);
-    const dim3 grid((unsigned)(((rows + BM - 1) / BM) * (a.cout / bn)));
+    // BN 256: 224-row tiles when that packs the rounds of one workgroup per
+    // CU better (64 ROIs: 961 tiles = 4 rounds of 224 rows instead of 841 =
+    // 4 rounds of 256, the last one 29 % full)
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    }
+    static const int bm_env = getenv("KPD_HMCONV_BM") ? atoi(getenv("KPD_HMCONV_BM")) : 0;   // A/B
+    auto cost = [&](long bm) { return ((rows + bm - 1) / bm * (a.cout / bn) + ncu - 1) / ncu * bm; };
+    const int bm = fin || bn != 256 ? BM : bm_env == 224 || bm_env == BM ? bm_env : (cost(224) < cost(BM) ? 224 : BM);
+    const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
     if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
+    else if (bn == 256 && bm == 224 && dbg == 0) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 1) hipLaunchKernelGGL((hmconv_kernel<256, 2, 1>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 2) hipLaunchKernelGGL((hmconv_kernel<256, 2, 2>), grid, dim3(NT), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2>), grid, dim3(NT), 0, st, a);
