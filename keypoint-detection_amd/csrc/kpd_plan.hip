@@ -1217,7 +1217,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
   const bool fin_fused = p->hm3.bf16 && p->hm3.cout_p == 64 && !no_fin_fuse;
   const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
-  if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr)) return rc;
+  if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr,
+                       take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
+    return rc;
   c3.reset();
   {
     Stage sg(p, "hm_final_decode", st);

@@ -30,7 +30,8 @@ def main():
         for _ in range(4):
             m(batch)
     torch.cuda.synchronize()
-    st = plan.debug_buffer("stamps_hm2").view(torch.int64).cpu().numpy().reshape(-1, 8)
+    name = sys.argv[1] if len(sys.argv) > 1 else "stamps_hm2"   # stamps_hm3: conv 3 (fused final)
+    st = plan.debug_buffer(name).view(torch.int64).cpu().numpy().reshape(-1, 8)
     st = st[st[:, 0] != 0]
     t = st[:, [0, 1, 2, 3]].astype(np.float64) * 0.01
     t -= t[:, 0].min()
