@@ -68,6 +68,17 @@ __device__ __forceinline__ float dpp_xor1(float x) {
 __device__ __forceinline__ float dpp_xor2(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
 }
+template <int N>
+__device__ __forceinline__ float dpp_row_ror(float x) {   // lane l <- lane (l + N) mod 16 of its 16-lane row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+}
+// 1 / (1 + e^-v) with the hardware reciprocal and one Newton step (within an
+// ulp or two of the IEEE quotient; the division sequence is ~10 instructions)
+__device__ __forceinline__ float sigmoid_rcp(float v) {
+  const float d = 1.f + expf(-v);
+  const float r = __builtin_amdgcn_rcpf(d);
+  return fmaf(r, fmaf(-d, r, 1.f), r);
+}
 __device__ __forceinline__ void quad_transpose(f32x4& v, int t) {
   const bool b0 = t & 1, b1 = t & 2;
   float r = dpp_xor1(b0 ? v[0] : v[1]);
@@ -1194,8 +1205,10 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        a[i] += __shfl_xor(a[i], 4);
-        a[i] += __shfl_xor(a[i], 8);
+        // sum over the 4 lanes of the row with the same (lane & 3): DPP row
+        // rotations by 4 and 8 (no LDS round trip as with a shuffle)
+        a[i] += dpp_row_ror<4>(a[i]);
+        a[i] += dpp_row_ror<8>(a[i]);
         o[i][k] = a[i];
       }
     }
@@ -1214,7 +1227,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
         if (s4 * 4 + 1 < NKF && q4 == 1) val = o[i][s4 * 4 + 1];
         if (s4 * 4 + 2 < NKF && q4 == 2) val = o[i][s4 * 4 + 2];
         if (s4 * 4 + 3 < NKF && q4 == 3) val = o[i][s4 * 4 + 3];
-        if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? kpd_sigmoid(val + fw[NKF * 64 + k]) : 0.f;
+        if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? sigmoid_rcp(val + fw[NKF * 64 + k]) : 0.f;
       }
     }
   }
