@@ -70,6 +70,9 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
   if (c < FC) {
     const float* src = staged ? sst : stats + (size_t)n * tiles * 2 * FC;
     float s = 0.f, m = -INFINITY;
+    // unrolled so the LDS reads of 16 tiles are in flight together (the adds
+    // stay in tile order)
+#pragma unroll 16
     for (int t = 0; t < tiles; ++t) {
       s += src[t * 2 * FC + c];
       m = fmaxf(m, src[t * 2 * FC + FC + c]);
@@ -82,6 +85,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
     const int j = c & 7;
     const float* vv = (c < 8) ? avg : mx;
     float a = b0[j];
+#pragma unroll 32
     for (int k = 0; k < FC; ++k) a = fmaf(sw0[j * FC + k], vv[k], a);
     h[c] = fmaxf(a, 0.f);
   }
@@ -97,6 +101,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
   __syncthreads();   // waves 2-3 (c >= 128) have exited: the barrier counts waves 0-1
   // rank = number of channels ordered before c (score desc, index asc on ties)
   int rank = 0;
+#pragma unroll 32
   for (int k = 0; k < FC; ++k) {
     const float o = sc[k];
     rank += (o > score) || (o == score && k < c);
