@@ -31,11 +31,13 @@ constexpr int FC = 128;             // FPN channels
 // partials and both FC weights are staged in LDS in one load round trip
 // (every load in flight before the first use); the sums then run in tile
 // order from LDS, as before.
+__device__ __forceinline__ void slotmap_image(const float* __restrict__ boxes, int b, int P, int32_t* __restrict__ slot);
 constexpr int kTopkMaxTiles = 144;   // LDS: tiles x 1 KB + 8 KB
 __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ stats, int tiles, int HW,
                                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                                    const float* __restrict__ w2, const float* __restrict__ b2,
-                                                   int32_t* __restrict__ topk, float* __restrict__ scores_out) {
+                                                   int32_t* __restrict__ topk, float* __restrict__ scores_out,
+                                                   const float* __restrict__ boxes, int P, int32_t* __restrict__ slot) {
   extern __shared__ __attribute__((aligned(16))) float tsm[];
   // more tiles than fit in LDS (the fp32 path's small tiles at 384x288):
   // the partials are summed straight from global memory
@@ -90,7 +92,12 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
     h[c] = fmaxf(a, 0.f);
   }
   __syncthreads();
-  if (c >= FC) return;
+  if (c >= FC) {
+    // (optional) the image's box slot map (slotmap_kernel's work) on a thread
+    // of the otherwise idle upper waves: one launch less per forward
+    if (slot && c == 255) slotmap_image(boxes, n, P, slot);
+    return;
+  }
   float oa = b2[c], om = b2[c];
   for (int j = 0; j < 8; ++j) {
     oa = fmaf(sw2[c * 8 + j], h[j], oa);
@@ -113,9 +120,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
 // ---------------------------------------------------------------- slot map
 // One thread per image: compaction of non-zero boxes (keypoint_model.py:149-153),
 // and the "no valid person" dummy (vis class 0 = 1, :171-179).
-__global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, int32_t* __restrict__ slot) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+__device__ __forceinline__ void slotmap_image(const float* __restrict__ boxes, int b, int P, int32_t* __restrict__ slot) {
   int cnt = 0;
   for (int p = 0; p < P; ++p) {
     const float* bx = boxes + ((size_t)b * P + p) * 4;
@@ -132,6 +137,11 @@ __global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, in
       slot[b * P + p] = valid++;
     }
   }
+}
+__global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, int32_t* __restrict__ slot) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  slotmap_image(boxes, b, P, slot);
 }
 
 // ---------------------------------------------------------------- ROI align
@@ -492,9 +502,12 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
 }  // namespace
 
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
-                       const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st) {
+                       const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
+                       const float* boxes, int P, int32_t* slot) {
+  if (slot && (!boxes || P <= 0 || P > 0xFFFF)) return hipErrorInvalidValue;
   const size_t lds = ((size_t)(tiles <= kTopkMaxTiles ? tiles : 0) * 2 * FC + 2 * 8 * FC) * 4;
-  hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores);
+  hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores,
+                     boxes, P, slot);
   return hipGetLastError();
 }
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipStream_t st) {

@@ -1161,7 +1161,10 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   fpn_stage.reset();
   std::unique_ptr<Stage> topk_stage(new Stage(p, "topk", st));
   if (!d.fused_stats) HIP_TRY(launch_channel_stats(w.feat, B, HWf, 128, d.tiles, w.stats, st));
-  HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st));
+  // given boxes for every image: the slot map rides along with the top-k launch
+  const bool slot_in_topk = !detect && NB == B && NB * P > 0 && boxes != nullptr;
+  HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st,
+                      slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr));
   topk_stage.reset();
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
   dbg["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
@@ -1194,7 +1197,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   // hm_final_kernel, decode_kernel and kh_final_kernel through the slot map
   {
     Stage sg(p, "roi_align", st);
-    HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
+    if (!slot_in_topk) HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
   }
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
