@@ -177,7 +177,15 @@ class MultiPersonKeypointModel(nn.Module):
         if nb > B:
             raise ValueError(f"bboxes describe {nb} images but the batch has {B}")
         P = max(len(b) for b in boxes)
-        bt = torch.stack([b.to(dev, torch.float32) for b in boxes]).contiguous()   # [nb,P,4]
+        # boxes given as one [B,P,4] float32 device tensor: read in place (the
+        # per-image list above is views of it), no stack copy
+        bb = batch["bboxes"]
+        t3 = bb if isinstance(bb, torch.Tensor) else bb[0]
+        if (t3.dim() == 3 and t3.dtype == torch.float32 and t3.device == dev and t3.is_contiguous()
+                and t3.size(0) == nb and t3.size(1) == P):
+            bt = t3
+        else:
+            bt = torch.stack([b.to(dev, torch.float32) for b in boxes]).contiguous()   # [nb,P,4]
         if bt.dim() != 3 or bt.size(-1) != 4:
             raise ValueError(f"Invalid bboxes format: {tuple(bt.shape)}")
         out = self._run(plan, image, bt, nb, P, flags)
