@@ -155,7 +155,7 @@ def main():
     def step():
         out = m(batch)
         if gather:   # result collation over RCCL: P all_reduce(MAX) + kpt/vis all_gather
-            collate_outputs(out, B * world)
+            collate_outputs(out, B * world, max_persons=P)
         return out
 
     with torch.no_grad():

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
   // weights and bias at wave-uniform addresses (scalar loads); the two pixels
   // share each weight in one packed FMA
   f2 o[16];
-  float m_abs = 0.f;
+  float m_abs[PT] = {0.f, 0.f};
 #pragma unroll
   for (int co = 0; co < 16; ++co) {
     f2 a = f2{0.f, 0.f};
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
 #pragma unroll
     for (int u = 0; u < PT; ++u) {
       o[co][u] = kpd_act(a[u] + b[co], ACT_HSWISH);
-      if (live[u]) m_abs = fmaxf(m_abs, fabsf(o[co][u]));
+      if (live[u]) m_abs[u] = fmaxf(m_abs[u], fabsf(o[co][u]));
     }
   }
   // stage the block's 512 x 64-byte outputs in LDS (XOR-swizzled quads), then
@@ -101,14 +101,23 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ img
     const int i = q * 256 + t, px = i >> 2, qq = i & 3;
     if (px < npx) dst[i] = so[px * 4 + (qq ^ (px & 3))];
   }
-  if (amax) {   // max|tap0| for the split FPN scale bound (conv_glds.hip)
-    const float wm = wave_max(m_abs);
+  if (amax) {   // per-image max|tap0| for the split FPN scale (conv_glds.hip, fpn0x_kernel)
+    // the block's first image reduces over the workgroup; pixels of a later
+    // image (a block straddling an image boundary) publish one by one
+    const int HWo = Ho * Wo, nb = pix0 / HWo;
+    float mb = 0.f;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int pix = pix0 + u * 256 + t;
+      if (!live[u]) continue;
+      const int n = pix / HWo;
+      if (n == nb) mb = fmaxf(mb, m_abs[u]);
+      else amax_publish_img(amax, n, m_abs[u]);
+    }
+    const float wm = wave_max(mb);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      amax_publish(amax, bm);
-    }
+    if (threadIdx.x == 0) amax_publish_img(amax, nb, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
   }
 }
 
@@ -885,24 +894,30 @@ __global__ __launch_bounds__(256) void pw_small_kernel(const ConvArgs a) {
     }
   // C layout: col = lane & 15 (channel), row = 4 * (lane >> 4) + i (pixel)
   float* out = static_cast<float*>(a.out);
+  // per-image max|out| (split FPN scale): rows of the block's first image
+  // reduce over the workgroup, rows of a later image publish directly
+  const int nb = blockIdx.x * 64 / HW;
   float m_abs = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + g * 4 + i;
     if (m >= M) continue;
+    float mr = 0.f;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const float v = kpd_act(acc[nt][i] + bias[nt], a.act) + resv[nt][i];
       out[(size_t)m * a.out_cstride + n0 + nt * 16 + r] = v;
-      m_abs = fmaxf(m_abs, fabsf(v));
+      mr = fmaxf(mr, fabsf(v));
     }
+    if (a.amax && m / HW != nb) amax_publish_img(a.amax, m / HW, mr);
+    else m_abs = fmaxf(m_abs, mr);
   }
   if (a.amax) {
     __shared__ float red[4];
     const float wm = wave_max(m_abs);
     if (lane == 0) red[wave] = wm;
     __syncthreads();
-    if (tid == 0) amax_publish(a.amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    if (tid == 0) amax_publish_img(a.amax, nb, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
   }
 }
 
@@ -1193,9 +1208,9 @@ __global__ __launch_bounds__(kSeThreads) void se_kernel(const float* __restrict_
 // channels of kLatPix pixels, all their inputs are loaded before the first
 // store, and every store is 16 bytes.  Weights transposed in LDS once per
 // workgroup; the grid is capped (kLatBlocks) and each workgroup strides over
-// chunks of 16 x kLatPix pixels, so the weight staging, the barrier and the
-// amax publish are amortised over many chunks.  Split output (sc_in != null): x * 2^a_exp as f16 hi + lo,
-// 32 channels per [hi32 | lo32] 128-byte group (the split FPN conv's K row).
+// chunks of 16 x kLatPix pixels, so the weight staging and the barrier are
+// amortised over many chunks.  fp32 FPN level 0 only: the split (mixed)
+// precision never materialises lateral 0 (fpn0x_kernel works by linearity).
 constexpr int kLatPix = 2;   // pixels per thread (4 doubles the registers and halves occupancy: slower)
 constexpr int kLatBlocks = 2048;
 template <int CIN4>          // cin_p / 4
@@ -1203,15 +1218,10 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ res, int H, int W, int rh,
-                                                             int rw, int M, float* __restrict__ out,
-                                                             float* __restrict__ amax, const float* __restrict__ sc_in,
-                                                             float maxb, float maxs, int nt_store) {
+                                                             int rw, int M, float* __restrict__ out, int nt_store) {
   __shared__ __attribute__((aligned(16))) float sw[32 * 128];
-  __shared__ float red[4];
   const int tid = threadIdx.x;
   constexpr int cin_p = CIN4 * 4;
-  float sa = 1.f;
-  if (sc_in) sa = ldexpf(1.f, split_a_exp(sc_in, maxb, maxs));
   for (int i = tid; i < cin_p * 128; i += 256) {
     const int co = i / cin_p, k = i - co * cin_p;
     sw[k * 128 + co] = w[i];
@@ -1221,7 +1231,6 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
   const float4 b0 = *reinterpret_cast<const float4*>(bias + co), b1 = *reinterpret_cast<const float4*>(bias + co + 4);
   const int HW = H * W;
   const float sy = (float)rh / (float)H, sx = (float)rw / (float)W;
-  float m_abs = 0.f;
   const int chunks = (M + 16 * kLatPix - 1) / (16 * kLatPix);
   for (int chunk = blockIdx.x; chunk < chunks; chunk += gridDim.x) {
     // load phase: inputs and residuals of this thread's pixels
@@ -1267,39 +1276,14 @@ __global__ __launch_bounds__(256) void lateral_stream_kernel(const float* __rest
       }
       a[0] += r0[it].x; a[1] += r0[it].y; a[2] += r0[it].z; a[3] += r0[it].w;
       a[4] += r1[it].x; a[5] += r1[it].y; a[6] += r1[it].z; a[7] += r1[it].w;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m_abs = fmaxf(m_abs, fabsf(a[e]));
-      if (sc_in) {
-        typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
-        f16x8v hi, lo;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xsc = a[e] * sa;
-          hi[e] = (_Float16)xsc;
-          lo[e] = (_Float16)(xsc - (float)hi[e]);
-        }
-        _Float16* o16 = reinterpret_cast<_Float16*>(out) + (size_t)m * 256 + (co >> 5) * 64 + (co & 31);
-        if (nt_store) {   // streamed past the caches (the 400 MB output exceeds L2 + MALL)
-          __builtin_nontemporal_store(hi, reinterpret_cast<f16x8v*>(o16));
-          __builtin_nontemporal_store(lo, reinterpret_cast<f16x8v*>(o16 + 32));
-        } else {
-          *reinterpret_cast<f16x8v*>(o16) = hi;
-          *reinterpret_cast<f16x8v*>(o16 + 32) = lo;
-        }
+      float* op = out + (size_t)m * 128 + co;
+      if (nt_store) {   // streamed past the caches (KPD_LAT_NT, A/B)
+        __builtin_nontemporal_store(f32x4{a[0], a[1], a[2], a[3]}, reinterpret_cast<f32x4*>(op));
+        __builtin_nontemporal_store(f32x4{a[4], a[5], a[6], a[7]}, reinterpret_cast<f32x4*>(op + 4));
       } else {
-        float* op = out + (size_t)m * 128 + co;
         *reinterpret_cast<float4*>(op) = make_float4(a[0], a[1], a[2], a[3]);
         *reinterpret_cast<float4*>(op + 4) = make_float4(a[4], a[5], a[6], a[7]);
       }
-    }
-  }
-  if (amax) {
-    const float wm = wave_max(m_abs);
-    if ((tid & 63) == 0) red[tid >> 6] = wm;
-    __syncthreads();
-    if (tid == 0) {
-      const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      amax_publish(amax, bm);
     }
   }
 }
@@ -1361,8 +1345,7 @@ hipError_t launch_se(const float* x, int N, int HW, int C, int Cp, const float* 
 }
 
 hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
-                                 int N, int H, int W, int rh, int rw, void* out, float* amax, const float* sc_in,
-                                 float maxb, float maxs, hipStream_t st) {
+                                 int N, int H, int W, int rh, int rw, void* out, hipStream_t st) {
   if (cin_p != 16 && cin_p != 32) return hipErrorInvalidValue;
   const int M = N * H * W;
   const int chunks = (M + 16 * kLatPix - 1) / (16 * kLatPix);
@@ -1370,7 +1353,7 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
   static const int nt_env = getenv("KPD_LAT_NT") ? atoi(getenv("KPD_LAT_NT")) : 0;
   const int nblk = std::max(1, std::min(chunks, blocks_env));
 #define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3(nblk), dim3(256), 0, st, in, w, bias, res, H, \
-                                  W, rh, rw, M, static_cast<float*>(out), amax, sc_in, maxb, maxs, nt_env)
+                                  W, rh, rw, M, static_cast<float*>(out), nt_env)
   switch (cin_p / 4) {
     case 4: LAT(4); break;
     case 8: LAT(8); break;

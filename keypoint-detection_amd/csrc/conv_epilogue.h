@@ -11,7 +11,7 @@ struct EpiArgs {
   void* out;           // NHWC rows of out_cstride elements
   const float* res;    // optional residual NHWC [N][rh][rw][cout_p] (nearest-upsampled when rh != H)
   float* stats;        // optional [N][tiles_per_img][2][cout_p] (requires HW % BM == 0)
-  float* amax;         // optional max|out| (slotted, amax_publish)
+  float* amax;         // optional per-image max|out| (amax_publish_img)
   float scale;         // acc multiplier before bias (split16 unscale), 1 otherwise
   int M, H, W, cout_p, out_cstride, rh, rw, act, tiles_per_img;
   // optional second per-channel affine after the activation (an un-foldable BN
@@ -129,18 +129,23 @@ __device__ __forceinline__ void tile_store(float* tile, const EpiArgs& p, int m0
     }
     v[it] = x;
   }
+  // per-image max|out|: cells of the tile's first image reduce over the
+  // wave, cells of a later image (a tile straddling images) publish directly
+  const int nb = m0 / HW;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int row = row0 + it * RS, m = m0 + row;
     if (m >= p.M || !col_ok) continue;
     const float4 x = v[it];
-    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    const float mc = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+    if (p.amax && m / HW != nb) amax_publish_img(p.amax, m / HW, mc);
+    else amax = fmaxf(amax, mc);
     store4<TO>(out + (size_t)m * p.out_cstride + co, x);
     if (p.stats) *reinterpret_cast<float4*>(tile + row * P + c4 * 4) = x;
   }
   if (p.amax) {
     const float w = wave_max(amax);
-    if ((tid & 63) == 0) amax_publish(p.amax, w);
+    if ((tid & 63) == 0) amax_publish_img(p.amax, nb, w);
   }
   if (p.stats) {
     // column sums / maxima: NT/BN row groups in parallel, then one combine

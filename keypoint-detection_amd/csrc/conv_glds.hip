@@ -69,15 +69,34 @@ __device__ __forceinline__ float dpp_xor2(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
 }
 template <int N>
-__device__ __forceinline__ float dpp_row_ror(float x) {   // lane l <- lane (l + N) mod 16 of its 16-lane row
+__device__ __forceinline__ float dpp_row_ror(float x) {   // row rotate right: lane l <- lane (l - N) mod 16
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+}
+// x + (lane l ^ 4) + (lane l ^ 8) + (lane l ^ 12) within a 16-lane row as a
+// symmetric butterfly: every lane of the group computes (x_a + x_b) + (x_c +
+// x_d) with the same pairs, so the sum is bit-identical in all four lanes and
+// does not depend on which lane a pixel landed in (a rotation sum associates
+// differently per lane: a result would then depend on the pixel's position in
+// the tile, i.e. on what the ROI is batched with).  xor 4 = ror 4 or ror 12
+// by bit 2 of the lane (l ^ 4 = l - 4 when bit 2 is set); xor 8 = ror 8.
+// Both rotations run unconditionally with the whole wave active and a plain
+// select picks one: a DPP inside a divergent branch reads the inactive lanes
+// of the other side as 0.
+__device__ __forceinline__ float dpp_sum_xor4_8(float x, int lane) {
+  const float r4 = dpp_row_ror<4>(x), r12 = dpp_row_ror<12>(x);
+  const unsigned sel = 0u - (unsigned)((lane >> 2) & 1);
+  const float u = __uint_as_float((__float_as_uint(r4) & sel) | (__float_as_uint(r12) & ~sel));
+  const float s = x + u;
+  return s + dpp_row_ror<8>(s);
 }
 // 1 / (1 + e^-v) with the hardware reciprocal and one Newton step (within an
 // ulp or two of the IEEE quotient; the division sequence is ~10 instructions)
+// For v < ~-88, e^-v overflows: d = inf, rcp = 0 and the Newton step would
+// give 0 * (1 - inf * 0) = NaN, so that case returns 0 like 1 / inf does.
 __device__ __forceinline__ float sigmoid_rcp(float v) {
   const float d = 1.f + expf(-v);
   const float r = __builtin_amdgcn_rcpf(d);
-  return fmaf(r, fmaf(-d, r, 1.f), r);
+  return d < INFINITY ? fmaf(r, fmaf(-d, r, 1.f), r) : 0.f;
 }
 __device__ __forceinline__ void quad_transpose(f32x4& v, int t) {
   const bool b0 = t & 1, b1 = t & 2;
@@ -380,7 +399,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 
   // ---------------- epilogue ----------------
   float scale = 1.f;
-  if constexpr (SPLIT) scale = ldexpf(1.f, -(split_a_exp(p.sc_in, p.sc_maxb, p.sc_maxs) + p.w_exp));
+  if constexpr (SPLIT) scale = p.split_scale;
   if constexpr (STAGED) {
     EpiArgs e;
     e.bias = p.bias; e.out = p.out; e.res = nullptr; e.stats = p.stats; e.amax = nullptr; e.scale = scale;
@@ -565,7 +584,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int STAGE = (BM + BN) * ROWB, RING = S * STAGE;
   // ring | stats exchange [2][WAVES_M][BN] | bias [BN] | class tables (ng, woff, g[4]) x 16
   constexpr int SMISC = RING + 2 * WAVES_M * BN * 4;
-  constexpr int LDS = SMISC + BN * 4 + 16 * 6 * 4;
+  constexpr int LDS = SMISC + BN * 4 + 16 * 6 * 4 + kFpn0xMaxImg * 4;   // + per-image unscale
   static_assert(LDS <= 160 * 1024, "LDS budget");
   constexpr int KT0 = 5;                          // tap0 K-tiles: taps (2k, 2k+1)
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -610,11 +629,15 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
 #pragma unroll
     for (int gi = 0; gi < kFpn0xMaxGroups; ++gi) s_g[tid * 4 + gi] = p.cls_g[tid][gi];
   }
-  float scale;
-  {
+  // unscale 2^-P of the split products, per image (from that image's own
+  // max|tap0| and max|lateral 1|): a table in LDS for the whole launch, so
+  // no global load enters the K loop's counted vmcnt waits
+  float* s_unscale = reinterpret_cast<float*>(lds + SMISC + BN * 4 + 16 * 6 * 4);
+  for (int u = tid; u < p.N; u += NT) {
     int a_f, a_l, P;
-    fpn0x_exps_from(fpn0x_slots(p.sc), p.w_exp0, p.w_expE, &a_f, &a_l, &P);
-    scale = ldexpf(1.f, -P);
+    fpn0x_exps(p.sc[(size_t)u * kAmaxStride], p.sc[(size_t)(p.sc_n + u) * kAmaxStride], p.w_exp0, p.w_expE, &a_f,
+               &a_l, &P);
+    s_unscale[u] = ldexpf(1.f, -P);
   }
   __syncthreads();
   // this lane's 16-byte piece of a tap0 K-row: chunks 0-1 hi(t1), 2-3 hi(t2),
@@ -759,6 +782,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   if (L >= ntiles) return;
   setup(L);
   rows(L, f_off, l_off, mask);
+  float scale = s_unscale[n], nscale = scale;
   static_assert(KT0 >= S, "the prefetched K-tiles of the next tile are tap0 K-tiles");
   // Every round starts with its first S K-tiles issued: round 0 here, later
   // rounds by the previous round (two inside its K loop, one after it).
@@ -804,7 +828,10 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb1);
         __builtin_amdgcn_s_setprio(0);
-        if (kt == 0 && has_next) rows(Lnext, nf_off, nl_off, nmask);
+        if (kt == 0 && has_next) {
+          rows(Lnext, nf_off, nl_off, nmask);
+          nscale = s_unscale[(Lnext >> 4) / p.tpc];
+        }
         if (more) rd_b(ns, 1, fb1);
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb0);
@@ -821,7 +848,9 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     stamp16(p.stamps, 5, (unsigned long long)KT, L);
     // this tile's geometry for the epilogue; then the next tile's prologue
     const int e_cls = cls, e_n = n, e_jt = jt, e_ca = ca, e_cb = cb, e_q0 = q0;
+    const float e_scale = scale;
     if (has_next) {
+      scale = nscale;
       const int last = sb + KT - 1;   // the stage of this tile's last K-tile
       sb = (sb + KT) % S;
       setup(Lnext);
@@ -838,7 +867,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     stamp16(p.stamps, 6, 0, L);
 
     // ---------------- register epilogue ----------------
-    const int t4 = lane & 3, q4 = r16 >> 2;
+    const int t4 = lane & 3;
     float* sts = reinterpret_cast<float*>(lds + RING);
     const int row_lim = RG - (e_q0 + wm * WM + g * 4);
     const bool full = e_q0 + BM <= RG;
@@ -852,7 +881,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
-            const float v0 = fmaxf(acc[i][j][e] * scale + bj, 0.f), v1 = fmaxf(acc[i][j][e + 1] * scale + bj, 0.f);
+            const float v0 = fmaxf(acc[i][j][e] * e_scale + bj, 0.f), v1 = fmaxf(acc[i][j][e + 1] * e_scale + bj, 0.f);
             acc[i][j][e] = v0;
             acc[i][j][e + 1] = v1;
             sm += v0;
@@ -864,7 +893,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float v = fmaxf(acc[i][j][e] * scale + bj, 0.f);
+            const float v = fmaxf(acc[i][j][e] * e_scale + bj, 0.f);
             acc[i][j][e] = v;
             const bool row_ok = i * 16 + e < row_lim;
             sm += row_ok ? v : 0.f;
@@ -938,18 +967,19 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
 }
 
 // fp32 rows -> f16 hi|lo rows (groups of G = 32 channels, 16 when cin == 16),
-// scaled by the power of two of operand `which` (0: tap0, 1: lateral 1)
-__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ in, long npix, int cin,
+// pixel px of image px / hw scaled by that image's power of two for operand
+// `which` (0: tap0, 1: lateral 1) -- fpn0x_exps on the image's own maxima
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ in, int N, long hw, int cin,
                                                          const float* __restrict__ sc, int which, int w_exp0,
                                                          int w_expE, _Float16* __restrict__ out) {
-  int a_f, a_l, P;
-  fpn0x_exps(sc, w_exp0, w_expE, &a_f, &a_l, &P);
-  const float s = ldexpf(1.f, which ? a_l : a_f);
   const int G = cin == 16 ? 16 : 32, c8n = cin / 8;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npix * c8n) return;
+  if (i >= (long)N * hw * c8n) return;
   const long px = i / c8n;
-  const int c = (int)(i - px * c8n) * 8;
+  const int c = (int)(i - px * c8n) * 8, n = (int)(px / hw);
+  int a_f, a_l, P;
+  fpn0x_exps(sc[(size_t)n * kAmaxStride], sc[(size_t)(N + n) * kAmaxStride], w_exp0, w_expE, &a_f, &a_l, &P);
+  const float s = ldexpf(1.f, which ? a_l : a_f);
   const float4 u = *reinterpret_cast<const float4*>(in + px * cin + c);
   const float4 v = *reinterpret_cast<const float4*>(in + px * cin + c + 4);
   const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
@@ -1205,10 +1235,9 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        // sum over the 4 lanes of the row with the same (lane & 3): DPP row
-        // rotations by 4 and 8 (no LDS round trip as with a shuffle)
-        a[i] += dpp_row_ror<4>(a[i]);
-        a[i] += dpp_row_ror<8>(a[i]);
+        // sum over the 4 lanes of the row with the same (lane & 3): DPP
+        // butterfly (no LDS round trip as with a shuffle), lane-symmetric
+        a[i] = dpp_sum_xor4_8(a[i], lane);
         o[i][k] = a[i];
       }
     }
@@ -1275,8 +1304,8 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
   if (a.M <= 0) return hipSuccess;
   if (a.cin_e % 64 != 0 || a.in_cstride % 8 != 0 || (a.stats && (a.H * a.W) % BM != 0))
     return hipErrorInvalidValue;
-  if (split) {
-    if (out_bf16 || a.cout_p != 128 || !a.sc_in) return hipErrorInvalidValue;
+  if (split) {   // diagnostics only (kpd_bench_conv16)
+    if (out_bf16 || a.cout_p != 128) return hipErrorInvalidValue;
     return launch<true, float, 3, 128, 3>(a, st);
   }
   if (a.cout_p % 256 == 0)
@@ -1340,6 +1369,7 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
 
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   if (a.N <= 0) return hipSuccess;
+  if (a.N > kFpn0xMaxImg || !a.sc || a.sc_n < a.N) return hipErrorInvalidValue;
   if (a.Hf != 4 * a.rh || a.Wf != 4 * a.rw || a.tpc != (a.rh * a.rw + BM - 1) / BM) return hipErrorInvalidValue;
   if ((long)a.tpc * BM >= 65536) return hipErrorInvalidValue;   // the kernel's float q / rw
   // 32-bit buffer offsets of the output and statistics stores
@@ -1364,11 +1394,11 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_split_rows(const float* in, long npix, int cin, const float* sc, int which, int w_exp0, int w_expE,
-                             void* out, hipStream_t st) {
+hipError_t launch_split_rows(const float* in, int N, long hw, int cin, const float* sc, int which, int w_exp0,
+                             int w_expE, void* out, hipStream_t st) {
   if (cin != 16 && cin % 32 != 0) return hipErrorInvalidValue;
-  const long n = npix * (cin / 8);
-  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, npix, cin, sc,
+  const long n = (long)N * hw * (cin / 8);
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, N, hw, cin, sc,
                      which, w_exp0, w_expE, static_cast<_Float16*>(out));
   return hipGetLastError();
 }
@@ -1394,21 +1424,20 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
   const int cin_e = split ? 2 * cin : cin;
   const long in_b = M * cin_e * 2, w_b = (long)cout * 9 * cin_e * 2, out_b = M * cout * 4;
   if (in_b > kMaxDesc) return -1;
-  void *in = nullptr, *wt = nullptr, *out = nullptr, *bias = nullptr, *sc = nullptr, *stats = nullptr;
+  void *in = nullptr, *wt = nullptr, *out = nullptr, *bias = nullptr, *stats = nullptr;
   const bool with_stats = split && ((long)H * W) % BM == 0;   // as FPN0 runs: top-k statistics fused
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = -2;
   if (hipMalloc(&in, in_b) != hipSuccess || hipMalloc(&wt, w_b) != hipSuccess || hipMalloc(&out, out_b) != hipSuccess ||
-      hipMalloc(&bias, cout * 4) != hipSuccess || hipMalloc(&sc, 2 * kAmaxSlots * kAmaxStride * 4) != hipSuccess ||
+      hipMalloc(&bias, cout * 4) != hipSuccess ||
       (with_stats && hipMalloc(&stats, (size_t)N * (H * W / BM) * 2 * cout * 4) != hipSuccess))
     goto done;
   (void)hipMemset(in, 0x3C, in_b);
   (void)hipMemset(wt, 0x3A, w_b);
   (void)hipMemset(bias, 0, cout * 4);
-  (void)hipMemset(sc, 0, 2 * kAmaxSlots * kAmaxStride * 4);
   a.in = in; a.wt = wt; a.bias = (const float*)bias; a.out = out; a.N = N; a.H = H; a.W = W; a.cin_e = cin_e;
   a.cout_p = cout; a.in_cstride = cin_e; a.out_cstride = cout; a.act = ACT_RELU; a.M = (int)M;
-  a.sc_in = (const float*)sc; a.sc_maxb = 1.f; a.sc_maxs = 1.f;
+  a.split_scale = 1.f;
   a.in_bytes = (int)in_b; a.wt_bytes = (int)w_b;
   if (with_stats) { a.stats = (float*)stats; a.tiles_per_img = H * W / BM; }
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) goto done;
@@ -1438,7 +1467,7 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
 done:
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
-  (void)hipFree(in); (void)hipFree(wt); (void)hipFree(out); (void)hipFree(bias); (void)hipFree(sc);
+  (void)hipFree(in); (void)hipFree(wt); (void)hipFree(out); (void)hipFree(bias);
   (void)hipFree(stats);
   return rc;
 }

@@ -268,7 +268,6 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const ConvArgs p) {
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
   const int C4 = p.cout_p / 4;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  float amax = 0.f;
   if (idx < (long)p.M * C4) {
     const int m = (int)(idx / C4), co = (int)(idx - (long)m * C4) * 4;
     const size_t slice = (size_t)p.M * p.cout_p, off = (size_t)m * p.cout_p + co;
@@ -298,12 +297,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
       x.x = kpd_act(x.x, p.act3); x.y = kpd_act(x.y, p.act3);
       x.z = kpd_act(x.z, p.act3); x.w = kpd_act(x.w, p.act3);
     }
-    amax = fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
     *reinterpret_cast<float4*>(static_cast<float*>(p.out) + (size_t)m * p.out_cstride + co) = x;
-  }
-  if (p.amax) {
-    const float w = wave_max(amax);
-    if ((threadIdx.x & 63) == 0) amax_publish(p.amax, w);
+    // per-image max|out| (split-K runs on maps of <= 256 pixels: few cells)
+    if (p.amax)
+      amax_publish_img(p.amax, m / (p.H * p.W), fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
   }
 }
 

@@ -18,7 +18,7 @@ struct ConvArgs {
   int act;
   int M;                 // N*H*W
   int tiles_per_img;
-  float* amax;           // optional: max|out| into kAmaxSlots slots (amax_publish; caller zeroes them)
+  float* amax;           // optional: per-image max|out|, slot n = amax[n * kAmaxStride] (amax_publish_img; caller zeroes)
   const float* post_scale;  // optional second affine after act (see conv_epilogue.h)
   const float* post_shift;
   int act2, act3;
@@ -41,10 +41,8 @@ struct Conv16Args {
   int N, H, W;
   int cin_e;             // 16-bit elements per tap row (cin, or 2*cin in split mode), % 64 == 0
   int cout_p, in_cstride, out_cstride, act, M, tiles_per_img;
-  // split mode: activation scale from the bound max|A| <= maxb + sc_in[0]*maxs + sc_in[1]
-  const float* sc_in;
-  float sc_maxb, sc_maxs;
-  int w_exp;
+  // split mode (kpd_bench_conv16 diagnostics only): products unscaled by split_scale
+  float split_scale;
   int in_bytes, wt_bytes;   // filled by the launcher
   // optional fused HeatmapHead final_layer (1x1 64->17 + sigmoid) for the
   // BN = 64 fp32-out conv: heatmap [B][P][17][H][W] at the ROI's slot
@@ -84,6 +82,7 @@ constexpr int kHmPad = 58;   // padded ROI side of the hmconv layout
 // read after the exact 4x nearest upsample].  Output pixels are processed by
 // class (y % 4, x % 4), so every MFMA row of a tile uses the same weights.
 constexpr int kFpn0xMaxGroups = 4;
+constexpr int kFpn0xMaxImg = 512;   // images per fpn0x launch (per-image unscale table in LDS)
 struct Fpn0xArgs {
   const void* f_split;     // tap0 as f16 [N][Hf][Wf][hi16 | lo16] (scale 2^a_f)
   const void* l_split;     // lateral 1 as f16 [N][rh][rw][4 x (hi32 | lo32)] (scale 2^a_l)
@@ -95,15 +94,17 @@ struct Fpn0xArgs {
   const float* bias;       // [128] (fpn conv + BN, folded)
   float* out;              // NHWC [N][Hf][Wf][128] fp32 (ReLU)
   float* stats;            // [N][16 * tpc][2][128] channel sum / max per tile
-  const float* sc;         // amax slots: max|tap0|, max|lat1|
+  const float* sc;         // per-image max|tap0| [sc_n] then max|lat1| [sc_n], stride kAmaxStride
+  int sc_n;                // images between the two slot arrays (>= N)
   int N, Hf, Wf, rh, rw, tpc, w_exp0, w_expE;
   int f_bytes, l_bytes, w0_bytes, weff_bytes;
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
-// fp32 NHWC -> f16 hi|lo split rows (groups of 32 channels, or 16 for cin 16)
-hipError_t launch_split_rows(const float* in, long npix, int cin, const float* sc, int which, int w_exp0, int w_expE,
-                             void* out, hipStream_t st);
+// fp32 NHWC -> f16 hi|lo split rows (groups of 32 channels, or 16 for cin 16),
+// each image scaled by its own power of two (per-image slots sc, see fpn0x_exps)
+hipError_t launch_split_rows(const float* in, int N, long hw, int cin, const float* sc, int which, int w_exp0,
+                             int w_expE, void* out, hipStream_t st);
 int conv16_tile_m();
 
 enum ConvDType : int { CONV_F32 = 0, CONV_BF16_OUT_BF16 = 1, CONV_BF16_OUT_F32 = 2 };
@@ -189,10 +190,8 @@ hipError_t launch_pw_small(const ConvArgs& a, hipStream_t st);
 hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st);
-// sc_in != null: split output (f16 [hi32|lo32] groups, scale from split_a_exp)
 hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
-                                 int N, int H, int W, int rh, int rw, void* out, float* amax, const float* sc_in,
-                                 float maxb, float maxs, hipStream_t st);
+                                 int N, int H, int W, int rh, int rw, void* out, hipStream_t st);
 
 // ---- channel attention / ROI / heatmap head / decode (head_kernels.hip) ----
 // slot != nullptr: also writes the slot map of boxes [N][P][4] (launch_slotmap's work)

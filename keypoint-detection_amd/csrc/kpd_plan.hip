@@ -120,7 +120,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
   float* pool = nullptr;    // [B][1024] SE channel means from the fused expand+depthwise kernel
   float* separt = nullptr;  // [B][kSePartFloats] SE fc1 partials (exdw_kernel -> seproj_kernel)
-  float* sc = nullptr;    // split FPN scale inputs: slotted max|tap0|, max|lateral1| (amax_publish)
+  float* sc = nullptr;    // split FPN scale inputs: per-image max|tap0| [B], max|lateral1| [B] (amax_publish_img)
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
   float* pd_head = nullptr;     // [B][56*56][48]
@@ -139,8 +139,12 @@ struct Dims {
   int h[12] = {}, w[12] = {};  // spatial dims after stem (0) and after bneck i (i+1)
   int Hf = 0, Wf = 0, tiles = 0;
   bool fused_stats = false;
-  bool operator==(const Dims& o) const {
-    return B == o.B && H == o.H && W == o.W && NB == o.NB && P == o.P && flags == o.flags;
+  // a workspace carved for `o` serves this pass: same geometry, no larger
+  // batch (kernels index by the pass's own B / NB / P; the zero borders of the
+  // padded heatmap maps are written once at carve time and never overwritten)
+  bool fits(const Dims& o) const {
+    return H == o.H && W == o.W && flags == o.flags && tiles == o.tiles && B <= o.B && NB <= o.NB && P <= o.P &&
+           (size_t)NB * P <= (size_t)o.NB * o.P;
   }
 };
 
@@ -163,11 +167,6 @@ struct kpd_plan {
   float *hca_w0 = nullptr, *hca_b0 = nullptr, *hca_w2 = nullptr, *hca_b2 = nullptr;
   float *sa_w = nullptr, *sa_b = nullptr;
   DevConv hm1, hm2, hm3;
-  struct {
-    _Float16* hl = nullptr;   // [128][9][4][hi32|lo32]
-    int w_exp = 0;
-    float maxb = 0.f, maxs = 0.f;
-  } fpn0s;  // split FPN level-0 weights
   struct {
     _Float16* w0 = nullptr;     // composite conv3x3.L0 weights [128][5][64]
     _Float16* weff = nullptr;   // per position class [128][groups][4][64]
@@ -343,51 +342,6 @@ int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& m
   return upload(p, w->data, out);
 }
 
-// Split weights for the FPN level-0 conv: downloads the packed fp32 weights
-// [cout_p][9][cin_p], scales by 2^w_exp so max|w| < 2^15 and splits every value
-// into f16 hi + lo, stored per 32 input channels as [hi32 | lo32] (the 128-byte
-// K-tile row of conv_glds.hip).  Also derives the constants of the device-side
-// bound max|lateral0| <= maxb + max|tap0| * maxs + max|lateral1| that fixes the
-// activation scale before lateral 0 is written (backbone.py:33-37: lateral0 =
-// conv1x1(tap0) + up(lateral1)).
-int pack_split16(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
-  const int cin = dc.cin_p;
-  if (cin % 32 != 0) return fail(KPD_EINVAL, "split FPN conv needs cin % 32 == 0");
-  const size_t n = (size_t)dc.cout_p * 9 * cin;
-  std::vector<float> w(n);
-  HIP_TRY(hipMemcpy(w.data(), dc.w, n * sizeof(float), hipMemcpyDeviceToHost));
-  float mx = 0.f;
-  for (float v : w) mx = std::max(mx, std::fabs(v));
-  int e = 0;
-  if (mx > 0.f) std::frexp(mx, &e);
-  const int w_exp = std::min(std::max(14 - e, -100), 100);
-  std::vector<_Float16> hl(2 * n);
-  for (size_t row = 0; row < (size_t)dc.cout_p * 9; ++row)
-    for (int ci = 0; ci < cin; ++ci) {
-      const float x = std::ldexp(w[row * cin + ci], w_exp);
-      const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
-      const size_t o = row * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
-      hl[o] = hi;
-      hl[o + 32] = lo;
-    }
-  if (int rc = upload(p, hl, &p->fpn0s.hl)) return rc;
-  p->fpn0s.w_exp = w_exp;
-  // lateral-0 bound constants (1x1 conv, [cout_p][cin_p] fp32 + bias)
-  std::vector<float> lw((size_t)lat0.cout_p * lat0.cin_p), lb(lat0.cout_p);
-  HIP_TRY(hipMemcpy(lw.data(), lat0.w, lw.size() * sizeof(float), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(lb.data(), lat0.b, lb.size() * sizeof(float), hipMemcpyDeviceToHost));
-  double maxb = 0.0, maxs = 0.0;
-  for (int co = 0; co < lat0.cout_p; ++co) {
-    double sa = 0.0;
-    for (int ci = 0; ci < lat0.cin_p; ++ci) sa += std::fabs((double)lw[(size_t)co * lat0.cin_p + ci]);
-    maxs = std::max(maxs, sa);
-    maxb = std::max(maxb, std::fabs((double)lb[co]));
-  }
-  p->fpn0s.maxb = (float)(maxb * (1.0 + 1e-6));
-  p->fpn0s.maxs = (float)(maxs * (1.0 + 1e-6));
-  return KPD_OK;
-}
-
 // FPN level 0 by linearity (fpn0x_kernel): W0 = W3 . L0 (the 3x3 conv on the
 // 16-channel stem tap through the bias-free lateral 0) and, per output position
 // class (y % 4, x % 4), the 3x3 taps summed by the lateral-1 pixel they read
@@ -528,7 +482,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   for (int i = 0; i < 4; ++i) w.lat[i] = c.take<float>((size_t)B * lh[i] * lw[i] * 128);
   w.feat = c.take<float>((size_t)B * d.Hf * d.Wf * 128);
   w.stats = c.take<float>((size_t)B * d.tiles * 2 * 128);
-  w.sc = c.take<float>(2 * kAmaxSlots * kAmaxStride);
+  w.sc = c.take<float>((size_t)2 * B * kAmaxStride);
   w.splitk = c.take<float>(kSplitKFloats);
   w.pool = c.take<float>((size_t)B * 1024);
   w.separt = c.take<float>((size_t)B * kSePartFloats);
@@ -729,7 +683,6 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   HIP_TRY(hipSetDevice(p->device));
   for (void* a : p->allocs) (void)hipFree(a);
   p->allocs.clear();
-  p->fpn0s.hl = nullptr;
   p->fpn0x.w0 = p->fpn0x.weff = nullptr;
   p->stamps = nullptr;
   p->pd = DevConv();
@@ -798,10 +751,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
-  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) {
-    chk(pack_split16(p, p->fpn0, p->lat[0]));
-    chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
-  }
+  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
@@ -902,8 +852,26 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   return KPD_OK;
 }
 
+// Images per forward pass: fpn0x_kernel's 32-bit store offsets (output and
+// tap0 / lateral-1 split rows) and its per-image unscale table bound the
+// batch one launch may cover; kpd_forward runs larger batches as several
+// passes (images are independent, so results do not depend on the split).
+static int max_pass_images(int H, int W) {
+  const long hf = (H - 1) / 2 + 1, wf = (W - 1) / 2 + 1;
+  const long by_extent = 0x7fffffffL / (hf * wf * 512);
+  return (int)std::max(1L, std::min<long>(kFpn0xMaxImg, by_extent));
+}
+
+// FPN level 0 by linearity applies (mixed precision, packed composite weights,
+// lateral 1 an exact 4x nearest upsample of the level-0 grid)
+static bool fpn0x_ok(const kpd_plan* p, const Dims& d) {
+  static const bool no_lin = getenv("KPD_NO_FPN0X") != nullptr;   // A/B switch
+  return p->precision == KPD_PRECISION_MIXED && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] &&
+         d.Wf == 4 * d.w[3] && (long)((d.h[3] * d.w[3] + 255) / 256) * 256 < 65536;
+}
+
 static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
-  if (p->have_work[k] && p->dims[k] == d) return KPD_OK;
+  if (p->have_work[k] && d.fits(p->dims[k])) return KPD_OK;
   Work w;
   const size_t need = carve(p, d, nullptr, w);
   if (need > p->ws_bytes[k]) {
@@ -937,12 +905,13 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     d.w[i + 1] = (d.w[i] + 2 * pd - k) / s + 1;
   }
   d.Hf = d.h[0]; d.Wf = d.w[0];
-  const bool split = p->precision == KPD_PRECISION_MIXED && p->fpn0s.hl != nullptr;
-  const int HWf = d.Hf * d.Wf, TM = split ? conv16_tile_m() : conv_tile_m();
-  // FPN level 0 by linearity when lateral 1 is an exact 4x nearest upsample
-  static const bool no_lin = getenv("KPD_NO_FPN0X") != nullptr;   // A/B switch
-  const bool lin = split && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] && d.Wf == 4 * d.w[3] &&
-                   (size_t)B * HWf * 64 < 0x7fffffffu;   // 31-bit buffer descriptors
+  const int HWf = d.Hf * d.Wf;
+  // split (fp32-accurate f16 hi + lo) FPN level 0 by linearity: when lateral 1
+  // is an exact 4x nearest upsample of the level-0 grid (kpd_forward caps the
+  // pass at max_pass_images, which keeps the 31-bit buffer extents); other
+  // geometries run the fp32 level-0 conv
+  const bool lin = fpn0x_ok(p, d) && B <= max_pass_images(H, W);
+  const int TM = conv_tile_m();
   const int tpc = (d.h[3] * d.w[3] + 255) / 256;   // fpn0x tiles per (position class, image)
   d.fused_stats = lin || (HWf % TM) == 0;
   d.tiles = lin ? 16 * tpc : (d.fused_stats ? HWf / TM : std::min(64, HWf));
@@ -971,8 +940,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
 
   // ---------------- MobileNetV3-Small body ----------------
   std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
-  if (split) HIP_TRY(hipMemsetAsync(w.sc, 0, 2 * kAmaxSlots * kAmaxStride * sizeof(float), st));
-  HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], split ? w.sc : nullptr, st));
+  if (lin) HIP_TRY(hipMemsetAsync(w.sc, 0, (size_t)2 * B * kAmaxStride * sizeof(float), st));
+  HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], lin ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
   for (int i = 0; i < 11; ++i) {
@@ -1108,21 +1077,20 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
     if (i == 0 && lin) {   // no lateral 0: tap0 and lateral 1 go to the split layouts fpn0x_kernel reads
       char* base = reinterpret_cast<char*>(w.lat[0]);
-      HIP_TRY(launch_split_rows(taps[0], (long)B * lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
+      HIP_TRY(launch_split_rows(taps[0], B, (long)lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
                                 base, st));
-      HIP_TRY(launch_split_rows(w.lat[1], (long)B * lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
+      HIP_TRY(launch_split_rows(w.lat[1], B, (long)lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
                                 p->fpn0x.w_expE, base + (size_t)B * lh[0] * lw[0] * 64, st));
       continue;
     }
     if (i == 0 && L.cin_p <= 32) {   // the 16-channel stem tap: a 403 MB/step stream, not a GEMM
       HIP_TRY(launch_lateral_stream(taps[0], L.cin_p, (const float*)L.w, L.b, res, B, lh[0], lw[0], lh[1], lw[1],
-                                    w.lat[0], nullptr, split ? w.sc : nullptr, p->fpn0s.maxb, p->fpn0s.maxs, st));
+                                    w.lat[0], st));
       continue;
     }
-    if (i == 0 && split) return fail(KPD_EINVAL, "split FPN needs the 16-channel stem tap");
     if (int rc = conv(L, taps[i], B, lh[i], lw[i], pad16(kFpnIn[i]), w.lat[i], ACT_NONE, res,
                       i < 3 ? lh[i + 1] : 0, i < 3 ? lw[i + 1] : 0, nullptr, nullptr, 0, 0, st,
-                      (i == 1 && split) ? w.sc + kAmaxSlots * kAmaxStride : nullptr))
+                      (i == 1 && lin) ? w.sc + (size_t)B * kAmaxStride : nullptr))
       return rc;
   }
   lat_stage.reset();
@@ -1138,7 +1106,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       a.cls_ng[c] = p->fpn0x.cls_ng[c];
       for (int g = 0; g < kFpn0xMaxGroups; ++g) a.cls_g[c][g] = p->fpn0x.cls_g[c][g];
     }
-    a.bias = p->fpn0.b; a.out = w.feat; a.stats = w.stats; a.sc = w.sc;
+    a.bias = p->fpn0.b; a.out = w.feat; a.stats = w.stats; a.sc = w.sc; a.sc_n = B;
     a.N = B; a.Hf = d.Hf; a.Wf = d.Wf; a.rh = lh[1]; a.rw = lw[1]; a.tpc = tpc;
     a.w_exp0 = p->fpn0x.w_exp0; a.w_expE = p->fpn0x.w_expE;
     a.f_bytes = (int)std::min<size_t>((size_t)B * lh[0] * lw[0] * 64, 0x7fffffff);
@@ -1146,14 +1114,6 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     a.w0_bytes = p->fpn0x.w0_bytes; a.weff_bytes = p->fpn0x.weff_bytes;
     a.stamps = take_stamps("stamps_fpn0x", (size_t)16 * B * tpc);
     HIP_TRY(launch_fpn0x(a, st));
-  } else if (split) {
-    Conv16Args a{};
-    a.in = w.lat[0]; a.wt = p->fpn0s.hl; a.bias = p->fpn0.b; a.out = w.feat;
-    a.stats = d.fused_stats ? w.stats : nullptr;
-    a.N = B; a.H = d.Hf; a.W = d.Wf; a.cin_e = 256; a.cout_p = 128; a.in_cstride = 256; a.out_cstride = 128;
-    a.act = ACT_RELU; a.M = B * HWf; a.tiles_per_img = d.tiles;
-    a.sc_in = w.sc; a.sc_maxb = p->fpn0s.maxb; a.sc_maxs = p->fpn0s.maxs; a.w_exp = p->fpn0s.w_exp;
-    HIP_TRY(launch_conv16(a, 1, 0, st));
   } else if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
                            d.fused_stats ? w.stats : nullptr, d.tiles, 0, st)) {
     return rc;
@@ -1301,31 +1261,42 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   // a large batch runs as S contiguous sub-batches on S streams: the many
   // small latency-bound launches of one sub-batch (MobileNet body, heads)
   // overlap the other's.  Sub-batch 0 uses the caller's stream; the others
-  // fork from it and join back before return.  Debug buffers need S == 1.
+  // fork from it and join back before return.  A sub-batch larger than
+  // max_pass_images runs as consecutive passes on its stream, reusing its
+  // workspace.  Debug buffers need one pass.
   constexpr int kMinSub = 16;
   const int S = std::max(1, std::min({p->streams, kpd_plan::kMaxSub, B / kMinSub}));
-  if (S == 1)
-    return forward_one(p, 0, true, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis,
-                       box_scores, topk_out, st);
+  const int cap = max_pass_images(H, W);
+  const size_t img_sz = (size_t)C * H * W, per_kp = (size_t)P * 17;
+  auto run = [&](int k, bool debug, int b0, int b1, hipStream_t sk) -> int {
+    const int nb = b1 - b0;
+    const int npass = (nb + cap - 1) / cap;
+    for (int q = 0; q < npass; ++q) {
+      const int c0 = b0 + (int)((long)nb * q / npass), c1 = b0 + (int)((long)nb * (q + 1) / npass);
+      const int cbox = std::max(0, std::min(NB, c1) - c0);
+      auto off = [&](float* ptr, size_t per) { return ptr ? ptr + (size_t)c0 * per : ptr; };
+      if (int rc = forward_one(p, k, debug && npass == 1, image + (size_t)c0 * img_sz, c1 - c0, C, H, W,
+                               cbox > 0 || detect ? off(boxes, (size_t)P * 4) : nullptr, cbox, P, flags,
+                               off(kpts, per_kp * 2), off(vis, per_kp * 3), off(heat, per_kp * 3136),
+                               off(kh_kpts, per_kp * 2), off(kh_vis, per_kp * 3), off(box_scores, (size_t)P),
+                               topk_out ? topk_out + (size_t)c0 * 64 : nullptr, sk))
+        return rc;
+    }
+    return KPD_OK;
+  };
+  if (S == 1) return run(0, true, 0, B, st);
   if (!p->fork_ev) HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   for (int k = 1; k < S; ++k) {
     if (!p->sub_st[k]) HIP_TRY(hipStreamCreateWithFlags(&p->sub_st[k], hipStreamNonBlocking));
     if (!p->join_ev[k]) HIP_TRY(hipEventCreateWithFlags(&p->join_ev[k], hipEventDisableTiming));
   }
   HIP_TRY(hipEventRecord(p->fork_ev, st));
-  const size_t img_sz = (size_t)C * H * W, per_kp = (size_t)P * 17;
   int rc = KPD_OK;
   for (int k = 0; k < S && rc == KPD_OK; ++k) {
-    const int b0 = (int)((long)B * k / S), b1 = (int)((long)B * (k + 1) / S), nb = b1 - b0;
-    const int nbox = std::max(0, std::min(NB, b1) - b0);
+    const int b0 = (int)((long)B * k / S), b1 = (int)((long)B * (k + 1) / S);
     hipStream_t sk = k ? p->sub_st[k] : st;
     if (k) HIP_TRY(hipStreamWaitEvent(sk, p->fork_ev, 0));
-    auto off = [&](float* q, size_t per) { return q ? q + (size_t)b0 * per : q; };
-    rc = forward_one(p, k, false, image + (size_t)b0 * img_sz, nb, C, H, W, nbox > 0 || detect ? off(boxes, (size_t)P * 4)
-                                                                                           : nullptr,
-                     nbox, P, flags, off(kpts, per_kp * 2), off(vis, per_kp * 3), off(heat, per_kp * 3136),
-                     off(kh_kpts, per_kp * 2), off(kh_vis, per_kp * 3), off(box_scores, (size_t)P),
-                     topk_out ? topk_out + (size_t)b0 * 64 : nullptr, sk);
+    rc = run(k, false, b0, b1, sk);
   }
   for (int k = 1; k < S; ++k) {
     HIP_TRY(hipEventRecord(p->join_ev[k], p->sub_st[k]));

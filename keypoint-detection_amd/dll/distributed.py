@@ -31,6 +31,8 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def global_max_persons(p_local: int, device, group=None) -> int:
+    """all_reduce(MAX) of the per-rank person count.  Blocks on a host copy of
+    the result; ``collate_outputs`` skips it whenever P is known up front."""
     t = torch.tensor([p_local], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return int(t.item())
@@ -50,34 +52,54 @@ def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
     counts = [shard_range(total, world, r) for r in range(world)]
     mx = max(b - a for a, b in counts)
-    buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    buf[: local.size(0)] = local
+    if local.size(0) == mx:
+        buf = local.contiguous()
+    else:
+        buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        buf[: local.size(0)] = local
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
 
 
 def collate_outputs(out: Dict[str, torch.Tensor], total: int, group=None,
-                    keys: Sequence[str] = ("keypoints", "visibilities")) -> Dict[str, torch.Tensor]:
-    """Pad this rank's outputs to the global person count and all-gather ``keys``."""
-    p = global_max_persons(out["keypoints"].size(1), out["keypoints"].device, group)
+                    keys: Sequence[str] = ("keypoints", "visibilities"),
+                    max_persons: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """Pad this rank's outputs to the global person count and all-gather ``keys``
+    (add "heatmap" to collate the [n,P,17,56,56] heatmaps too: 213 KB per
+    person).  ``max_persons``: the global padded person count when the caller
+    knows it (a sharded [B,P,4] box tensor: P on every rank; the detector:
+    max_persons) -- then no all_reduce and no host synchronisation happen."""
+    p = max_persons
+    if p is None:
+        p = global_max_persons(out["keypoints"].size(1), out["keypoints"].device, group)
     res = {}
     for k in keys:
         res[k] = gather_images(pad_persons(out[k], p), total, group)
     return res
 
 
-def sharded_forward(model, images: torch.Tensor, boxes: torch.Tensor, group=None,
+def sharded_forward(model, images: torch.Tensor, boxes: Optional[torch.Tensor], group=None,
                     keys: Sequence[str] = ("keypoints", "visibilities")) -> Dict[str, torch.Tensor]:
     """Run this rank's shard of a global batch and return the collated outputs
-    of the whole batch on every rank."""
+    of the whole batch on every rank.  ``boxes``: the global [B,P,4] box tensor
+    (every rank's shard keeps the padded width P, so the collation needs no
+    person-count exchange), or None for the person-detector branch (P =
+    ``model.max_persons``)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     a, b = shard_range(images.size(0), world, rank)
+    k = getattr(model, "num_keypoints", 17)
+    p = boxes.size(1) if boxes is not None else int(getattr(model, "max_persons", 5))
+    dev = images.device
     if b > a:
-        out = model({"image": images[a:b], "bboxes": boxes[a:b]})
-    else:   # more ranks than images: contribute an empty shard
-        k = getattr(model, "num_keypoints", 17)
-        out = {"keypoints": torch.zeros(0, 0, 1, k, 2, device=images.device),
-               "visibilities": torch.zeros(0, 0, 1, k, 3, device=images.device)}
-    return collate_outputs(out, images.size(0), group, keys)
+        out = model({"image": images[a:b], "bboxes": boxes[a:b]} if boxes is not None else images[a:b])
+    elif p == 0:   # empty shard of a batch without boxes: the reference's all-empty shapes (:123-135)
+        out = {"keypoints": torch.zeros(0, 1, k, 2, device=dev), "visibilities": torch.zeros(0, 1, k, device=dev),
+               "heatmap": torch.zeros(0, 1, k, 56, 56, device=dev)}
+    else:          # more ranks than images: contribute an empty shard
+        out = {"keypoints": torch.zeros(0, p, 1, k, 2, device=dev),
+               "visibilities": torch.zeros(0, p, 1, k, 3, device=dev),
+               "heatmap": torch.zeros(0, p, k, 56, 56, device=dev)}
+    # P = 0 (no box anywhere): every image returns one zero person
+    return collate_outputs(out, images.size(0), group, keys, max_persons=max(p, 1))

@@ -2,7 +2,7 @@
 the global person-count all_reduce and the result all_gather that bench.py /
 dll.distributed use over RCCL on the GPU node."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -10,12 +10,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _init(rank, world, store):
+    # file rendezvous: no TCP port to race for between parallel test runs
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
 
 
 class FakeModel:
@@ -34,9 +31,8 @@ class FakeModel:
         return {"keypoints": k.contiguous(), "visibilities": v}
 
 
-def _worker(rank, world, port, total, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, total, q):
+    _init(rank, world, store)
     try:
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "keypoint-detection_amd"))
@@ -55,8 +51,8 @@ def test_sharded_forward_gloo(total):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    store = os.path.join(tempfile.mkdtemp(), "store")
+    procs = [ctx.Process(target=_worker, args=(r, world, store, total, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -89,3 +85,69 @@ def test_shard_range_properties():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
             sizes = [b - a for a, b in rs]
             assert max(sizes) - min(sizes) <= 1
+
+
+class OracleModel:
+    """The CPU oracle (oracle/kpd_oracle.py, pinned to the reference's goldens)
+    as the model stand-in: the real sharded_forward / collation path with real
+    per-image outputs."""
+    num_keypoints = 17
+
+    def __init__(self, sd):
+        self.sd = sd
+
+    def __call__(self, batch):
+        from oracle import kpd_oracle as O
+        return O.forward(self.sd, batch)
+
+
+def _oracle_case():
+    from dll.configs import ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+    sd = synthetic_state_dict(MultiPersonKeypointModel(ModelConfig(), TrainingConfig()).state_dict(), seed=0)
+    images = synthetic_images(5, 3, 96, 64, seed=3)
+    boxes = synthetic_boxes(5, 3, seed=4)
+    boxes[1, 1] = 0.0          # a zero box mid-list (compacted, padded)
+    boxes[4] = 0.0             # an image without any box (dummy person)
+    return sd, images, boxes
+
+
+def _oracle_worker(rank, world, store, q):
+    _init(rank, world, store)
+    try:
+        import sys
+        root = os.path.join(os.path.dirname(__file__), "..")
+        sys.path[:0] = [root, os.path.join(root, "keypoint-detection_amd")]
+        from dll.distributed import sharded_forward
+        torch.set_num_threads(2)
+        sd, images, boxes = _oracle_case()
+        out = sharded_forward(OracleModel(sd), images, boxes, keys=("keypoints", "visibilities", "heatmap"))
+        q.put((rank, {k: v.clone() for k, v in out.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_forward_oracle_gloo():
+    """world_size 2: the collated outputs of the sharded batch equal the
+    single-process forward of the whole batch (images are independent)."""
+    from oracle import kpd_oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    store = os.path.join(tempfile.mkdtemp(), "store")
+    procs = [ctx.Process(target=_oracle_worker, args=(r, world, store, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sd, images, boxes = _oracle_case()
+    ref = O.forward(sd, {"image": images, "bboxes": boxes})
+    for rank in range(world):
+        for k in ("keypoints", "visibilities", "heatmap"):
+            assert res[rank][k].shape == ref[k].shape, k
+            torch.testing.assert_close(res[rank][k], ref[k], atol=1e-5, rtol=0)
+    assert torch.equal(res[0]["visibilities"], res[1]["visibilities"])
+    assert res[0]["visibilities"][4, 0, 0, :, 0].eq(1).all()    # dummy person: visibility class 0

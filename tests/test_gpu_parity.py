@@ -149,18 +149,26 @@ def test_roi_features_vs_oracle(model_sd):
         np.testing.assert_allclose(roi[r].numpy(), want.numpy(), atol=2e-5)
 
 
-def test_batch_independence(model_sd):
-    """Images are independent: a batch equals its images run one at a time."""
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_batch_independence(model_sd, precision):
+    """Images are independent: a batch equals its images run one at a time,
+    bit for bit in every precision (the split FPN scale is per image)."""
     from dll.models.synthetic import synthetic_boxes, synthetic_images
     img = synthetic_images(6, 3, 256, 192, seed=31, device=DEV)
+    img[3] *= 4.0                            # one image with a larger dynamic range
     boxes = synthetic_boxes(6, 2, seed=32, device=DEV)
-    m = _model(model_sd)
+    m = _model(model_sd, precision)
     with torch.no_grad():
         full = m({"image": img, "bboxes": boxes})
         for i in (0, 3, 5):
             one = m({"image": img[i:i + 1], "bboxes": boxes[i:i + 1]})
             assert torch.equal(one["keypoints"][0], full["keypoints"][i])
             assert torch.equal(one["heatmap"][0], full["heatmap"][i])
+    assert torch.isfinite(full["heatmap"]).all()
+    ref = O.forward(model_sd, {"image": img[3:4].cpu(), "bboxes": boxes[3:4].cpu()})
+    tol_k, tol_h = (1e-5, 5e-5) if precision == "fp32" else (1e-3, 3e-2)
+    np.testing.assert_allclose(full["keypoints"][3:4].cpu().numpy(), ref["keypoints"].numpy(), atol=tol_k)
+    np.testing.assert_allclose(full["heatmap"][3:4].cpu().numpy(), ref["heatmap"].numpy(), atol=tol_h)
 
 
 def test_bench_batch_properties(model_sd):
@@ -176,8 +184,14 @@ def test_bench_batch_properties(model_sd):
     vis = out["visibilities"].cpu()
     assert kp.shape == (64, 1, 1, 17, 2) and ((kp >= 0) & (kp <= 1)).all()
     assert torch.equal(vis.sum(-1), torch.ones(64, 1, 1, 17))
-    ref = O.forward(model_sd, {"image": img[:2], "bboxes": boxes[:2]})
-    np.testing.assert_allclose(kp[:2].numpy(), ref["keypoints"].numpy(), atol=1e-3)
+    # every image of the bench batch against the oracle (the CPU restatement
+    # takes ~1 s for 64 images); mixed tolerances as in the module docstring
+    ref = O.forward(model_sd, {"image": img, "bboxes": boxes}, return_debug=True)
+    np.testing.assert_allclose(kp.numpy(), ref["keypoints"].numpy(), atol=1e-3)
+    flips = int((vis != ref["visibilities"]).any(dim=-1).sum())
+    assert flips <= 0.02 * 64 * 17
+    topk = m.native_plan(DEV).debug_buffer("scores").view(64, 128).cpu().topk(64, dim=1).indices
+    assert torch.equal(topk, ref["_topk"])
 
 
 def test_nms_gpu_vs_golden(golden_dir):
@@ -271,7 +285,7 @@ def test_predict_cli(tmp_path, capsys):
 @pytest.mark.parametrize("precision", ["fp32", "mixed"])
 def test_sub_batch_streams_match(model_sd, precision):
     """kpd_forward splits B >= 32 over sub-batch streams: same outputs as one
-    stream (bit-identical in fp32; the mixed FPN scale is per sub-batch)."""
+    stream, bit for bit in every precision (the split FPN scale is per image)."""
     from dll.models.synthetic import synthetic_boxes, synthetic_images
     img = synthetic_images(48, 3, 256, 192, seed=41, device=DEV)
     boxes = synthetic_boxes(48, 2, seed=42, device=DEV)
@@ -283,14 +297,8 @@ def test_sub_batch_streams_match(model_sd, precision):
         with torch.no_grad():
             outs.append(m({"image": img, "bboxes": boxes}))
     a, b = outs
-    if precision == "fp32":
-        assert torch.equal(a["keypoints"], b["keypoints"]) and torch.equal(a["heatmap"], b["heatmap"])
-        assert torch.equal(a["visibilities"], b["visibilities"])
-    else:
-        # the split FPN scale is per sub-batch: ~1e-7 relative in feat0, which the
-        # bf16 heatmap head can turn into a bf16 ulp here and there
-        torch.testing.assert_close(a["keypoints"], b["keypoints"], atol=1e-3, rtol=0)
-        torch.testing.assert_close(a["heatmap"], b["heatmap"], atol=3e-2, rtol=0)
+    assert torch.equal(a["keypoints"], b["keypoints"]) and torch.equal(a["heatmap"], b["heatmap"])
+    assert torch.equal(a["visibilities"], b["visibilities"])
 
 
 @pytest.mark.parametrize("precision", ["fp32", "mixed"])
@@ -316,3 +324,52 @@ def test_c5_shape_dual_head_vs_oracle(precision):
         assert flips <= 0.02
     np.testing.assert_allclose(out["kh_keypoints"].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol_k)
     np.testing.assert_allclose(out["kh_visibilities"].cpu().numpy(), ref["kh_visibilities"].numpy(), atol=tol_k)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "mixed"])
+def test_c4_rank_shard_bit_identical(precision):
+    """BASELINE C4's per-rank workload on one GPU: rank 3's shard of a
+    2048-image batch (shard_range(2048, 8, 3) = 256 images, 256x192), person
+    detector + NMS + dual head.  Every image's outputs are bit-identical when
+    the same images run as other shards / batch sizes (an 8-rank
+    sharded run equals the 1-rank run per image)."""
+    from dll.distributed import shard_range
+    from dll.models.synthetic import synthetic_images
+    a0, b0 = shard_range(2048, 8, 3)
+    assert (a0, b0) == (768, 1024)
+    m, sd = _dual_model(precision)
+    m.streams = 2
+    img = synthetic_images(b0 - a0, 3, 256, 192, seed=70 + a0, device=DEV)
+    img[17] *= 25.0                           # dynamic-range outlier inside the shard
+    with torch.no_grad():
+        full = m(img)
+        parts = [m(img[a:b]) for a, b in ((0, 37), (37, 38), (38, 160), (160, 256))]
+    keys = ("keypoints", "visibilities", "heatmap", "kh_keypoints", "kh_visibilities", "box_scores")
+    for k in keys:
+        got = torch.cat([p[k] for p in parts], dim=0)
+        assert torch.equal(got, full[k]), k
+    assert torch.equal(torch.stack([b for p in parts for b in p["boxes"]]), torch.stack(full["boxes"]))
+    assert full["keypoints"].shape == (256, 5, 1, 17, 2)
+    # a few images against the oracle on the detected boxes
+    ref = O.forward(sd, {"image": img[:3].cpu(), "bboxes": torch.stack(full["boxes"][:3]).cpu()}, dual_head=True)
+    tol = 1e-5 if precision == "fp32" else 1e-3
+    np.testing.assert_allclose(full["keypoints"][:3].cpu().numpy(), ref["keypoints"].numpy(), atol=tol)
+    np.testing.assert_allclose(full["kh_keypoints"][:3].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol)
+
+
+def test_saturated_heatmaps_finite(model_sd):
+    """An image scaled x40 drives heatmap logits far into the sigmoid's
+    saturation (e^-v overflows): every precision returns finite heatmaps in
+    [0, 1] and finite keypoints (the fused mixed-precision sigmoid once gave
+    NaN there).  The channel scores saturate too, so top-k ties make the
+    oracle comparison ill-posed here; only the invariants are checked."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(2, 3, 256, 192, seed=31, device=DEV) * 40.0
+    boxes = synthetic_boxes(2, 2, seed=32, device=DEV)
+    for precision in ("fp32", "mixed"):
+        m = _model(model_sd, precision)
+        with torch.no_grad():
+            out = m({"image": img, "bboxes": boxes})
+        h = out["heatmap"]
+        assert torch.isfinite(h).all() and (h >= 0).all() and (h <= 1).all(), precision
+        assert torch.isfinite(out["keypoints"]).all(), precision

@@ -1,0 +1,41 @@
+"""Diagnostic: where does a batched forward differ from single-image runs?
+Prints per-stage max |diff| (feat0, roi features, heatmaps) for a few images."""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "keypoint-detection_amd")]
+import torch  # noqa: E402
+
+from dll.configs import ModelConfig, TrainingConfig  # noqa: E402
+from dll.models import MultiPersonKeypointModel  # noqa: E402
+from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict  # noqa: E402
+
+prec = sys.argv[1] if len(sys.argv) > 1 else "mixed"
+dev = torch.device("cuda:0")
+m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=prec)
+m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
+m = m.to(dev).eval()
+B = 6
+img = synthetic_images(B, 3, 256, 192, seed=31, device=dev)
+img[3] *= 40.0
+boxes = synthetic_boxes(B, 2, seed=32, device=dev)
+with torch.no_grad():
+    full = m({"image": img, "bboxes": boxes})
+    plan = m.native_plan(dev)
+    f_full = plan.debug_buffer("feat0").view(B, -1).clone()
+    r_full = plan.debug_buffer("roi").view(B * 2, -1).clone()
+    for i in (0, 3, 5):
+        one = m({"image": img[i:i + 1], "bboxes": boxes[i:i + 1]})
+        f1 = plan.debug_buffer("feat0").view(1, -1)
+        r1 = plan.debug_buffer("roi").view(2, -1)
+        dh = (one["heatmap"][0] - full["heatmap"][i]).abs()
+        nz = dh.nonzero()
+        print(f"img {i}: feat0 {float((f1[0] - f_full[i]).abs().max()):.3e} "
+              f"roi {float((r1 - r_full[2 * i:2 * i + 2]).abs().max()):.3e} "
+              f"heat {float(dh.max()):.3e} ndiff {nz.shape[0]} "
+              f"kp {float((one['keypoints'][0] - full['keypoints'][i]).abs().max()):.3e}")
+        if nz.shape[0]:
+            print("   first diffs (p,k,y,x):", nz[:8].tolist())
+            print("   y range", int(nz[:, 2].min()), int(nz[:, 2].max()), "x range", int(nz[:, 3].min()),
+                  int(nz[:, 3].max()), "persons", sorted(set(nz[:, 0].tolist())), "kps", sorted(set(nz[:, 1].tolist()))[:5])
