@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=192)
     ap.add_argument("--persons", type=int, default=1)
-    ap.add_argument("--precision", default="mixed", choices=["fp32", "mixed"])
+    ap.add_argument("--precision", default="mixed", choices=["fp32", "split", "mixed"])
     ap.add_argument("--cpu-sample", type=int, default=8, help="images in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -40,6 +40,8 @@ extern "C" {
 
 #define KPD_PRECISION_FP32 0   /* every conv on fp32-input MFMA (exact fp32 products) */
 #define KPD_PRECISION_MIXED 1  /* heatmap-head convs on bf16 MFMA, fp32 accumulate; backbone fp32 */
+#define KPD_PRECISION_SPLIT 2  /* fp32-accurate: FPN level 0 and the heatmap-head convs as three
+                                  f16 MFMA products of hi/lo operand splits, fp32 accumulate */
 
 typedef struct kpd_plan kpd_plan;
 

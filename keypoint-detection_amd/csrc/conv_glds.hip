@@ -1020,7 +1020,7 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // DMA inside the K loop (the prologue's still lands)
 // BMH: GEMM rows per tile (256, or 224 so that the tile count packs the CUs'
 // rounds better -- launch_hmconv picks it; the window stays 384 rows)
-template <int BN, int SB, int DBG = 0, int BMH = BM>
+template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false>
 __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
@@ -1040,7 +1040,9 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   const int NTL = p.cout / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = HP + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
-  const int Mtot = p.R * HPP, cin = p.cin, NC = cin / 64, KT = 9 * NC;
+  // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
+  // channels as [hi32 | lo32] f16
+  const int Mtot = p.R * HPP, cin = p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = 9 * NC;
   stamp16(p.stamps, 0);
   const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
@@ -1050,13 +1052,13 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 - 64 + wave * (AWIN / 8) + i * 8 + lrow;
-    a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)(m * cin * 2 + lchunk * 16) : OOB;
+    a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)(m * RB + lchunk * 16) : OOB;
   }
   unsigned b_off[B_LD];
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) {
     const int co = n0 + wave * (BN / 8) + i * 8 + lrow;
-    b_off[i] = (unsigned)((co * 9 * cin) * 2 + lchunk * 16);
+    b_off[i] = (unsigned)(co * 9 * RB + lchunk * 16);
   }
   auto issue_a = [&](int c, int i) {   // A window of chunk c, wave-instruction i
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / 8) + i * 8) * ROWB);
@@ -1066,7 +1068,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     const int c = k / 9, t = k - c * 9;
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + wave * (BN / 8) * ROWB);
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], (t * cin + c * 64) * 2);
+    for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], t * RB + c * 128);
   };
   // Barrier of K-step k: B(k) landed.  A-window pieces are issued before the
   // B of the same batch, so every DMA younger than B(k) is among the
@@ -1126,40 +1128,119 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
       else if (i < 17 * 65) fin_pre[u] = p.fin_b[i - 17 * 64];
     }
   }
+  // SPLIT: per-ROI power-of-two scales of the tile's (at most two) ROIs,
+  // loaded before the K loop.  Input unscale 2^-(a_in + w_exp), output scale
+  // 2^a_out, a = split_exp_of(bound), bound = c + s * hsc[r][idx] (HmConvArgs).
+  const int rlo = m0 / HPP;                 // local ROI of the tile's first row (rows span <= 2 ROIs)
+  float us[2] = {1.f, 1.f}, os[2] = {1.f, 1.f};
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int rg = p.r0 + min(rlo + q, p.R - 1);
+      const float ui = p.in_c + p.in_s * p.hsc[(size_t)rg * 4 + p.in_idx];
+      us[q] = ldexpf(1.f, -(split_exp_of(ui) + p.w_exp));
+      if (p.out_idx >= 0) os[q] = ldexpf(1.f, split_exp_of(p.out_c + p.out_s * p.hsc[(size_t)rg * 4 + p.out_idx]));
+    }
+  }
+  const int rbound = (rlo + 1) * HPP;       // first padded position of the tile's second ROI
   // prologue: chunk 0's window and the first SB-1 K-steps' weights
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) issue_a(0, i);
 #pragma unroll
   for (int k = 0; k < SB - 1; ++k)
     if (k < KT) issue_b(k);
-  Half f0, f1;
   barrier_k(KT < SB - 1);
   stamp16(p.stamps, 1);
   if (NC > 1) issue_a(1, 0);
   if (SB - 1 < KT) issue_b(SB - 1);
-  load_half(0, 0, f0);
-  // K-step k: reads (k, q1) | MFMAs (k, q0) | barrier k+1 + DMA issue | reads (k+1, q0) | MFMAs (k, q1)
-  for (int k = 0; k < KT; ++k) {
-    load_half(k, 1, f1);
-    __builtin_amdgcn_s_setprio(1);
-    mma_half(f0);
-    __builtin_amdgcn_s_setprio(0);
-    if (k + 1 < KT) {
-      const int k1 = k + 1, c1 = k1 / 9, t1 = k1 - c1 * 9;
-      barrier_k(k1 + SB - 2 >= KT);   // B(k1) and its chunk's window landed; reads of k retired
-      if constexpr ((DBG & 2) == 0) {
-        if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);   // next chunk's window, spread over taps
-        if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);         // into the stage of B(k)
-      }
-      load_half(k1, 0, f0);
-    } else {
-      __builtin_amdgcn_s_waitcnt(0xC07F);
+  // DMA issue at barrier k1 (same schedule in both loops): the next chunk's
+  // window spread over this chunk's taps, and B(k1 + SB - 1) into the stage
+  // of B(k1 - 1), whose fragment reads every wave finished before barrier k1
+  auto issue_at = [&](int k1) {
+    if constexpr ((DBG & 2) == 0) {
+      const int c1 = k1 / 9, t1 = k1 - c1 * 9;
+      if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);
+      if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);
     }
-    // (threading the DMA pieces between the MFMA rows measured 2 % slower:
-    // the weights then land later than the next barrier wants them)
-    __builtin_amdgcn_s_setprio(1);
-    mma_half(f1);
-    __builtin_amdgcn_s_setprio(0);
+  };
+  if constexpr (!SPLIT) {
+    Half f0, f1;
+    load_half(0, 0, f0);
+    // K-step k: reads (k, q1) | MFMAs (k, q0) | barrier k+1 + DMA issue | reads (k+1, q0) | MFMAs (k, q1)
+    for (int k = 0; k < KT; ++k) {
+      load_half(k, 1, f1);
+      __builtin_amdgcn_s_setprio(1);
+      mma_half(f0);
+      __builtin_amdgcn_s_setprio(0);
+      if (k + 1 < KT) {
+        const int k1 = k + 1;
+        barrier_k(k1 + SB - 2 >= KT);   // B(k1) and its chunk's window landed; reads of k retired
+        issue_at(k1);
+        load_half(k1, 0, f0);
+      } else {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+      }
+      // (threading the DMA pieces between the MFMA rows measured 2 % slower:
+      // the weights then land later than the next barrier wants them)
+      __builtin_amdgcn_s_setprio(1);
+      mma_half(f1);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
+    // Split products per K-step: lo.hi | hi.hi | hi.lo (the lo.lo term, ~2^-22
+    // relative, is dropped) on v_mfma_f32_16x16x32_f16.  One fragment set;
+    // each register group is refilled with step k+1 as soon as its last pass
+    // of step k has issued, so every pass finds its operands read one or two
+    // passes earlier:  P1 al.bh | barrier k+1, DMA, read al' | P2 ah.bh |
+    // read bh' | P3 ah.bl | read ah', bl'.
+    uint4 ah[FM], al[FM], bh[FN], bl[FN];
+    auto rd_a = [&](int k, int q, uint4* f) {
+      const int c = k / 9, t = k - c * 9, off = (t / 3 - 1) * HP + (t % 3 - 1);
+      const char* ab = lds + (c & 1) * ABUF;
+      const int r0w = wm * WM + r16 + 64 + off;
+      const int ach = (((q ? 4 : 0) + g) ^ (r0w & 7)) << 4;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) f[i] = *reinterpret_cast<const uint4*>(ab + (r0w + i * 16) * ROWB + ach);
+    };
+    auto rd_b = [&](int k, int q, uint4* f) {
+      const char* bb = lds + 2 * ABUF + (k % SB) * BSTAGE;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
+    };
+    auto pass = [&](const uint4* a, const uint4* b) {
+      if constexpr ((DBG & 1) != 0) {
+        acc[0][0][0] += __uint_as_float(a[0].x ^ b[FN - 1].w);
+        return;
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, b[j]),
+                                                             acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    rd_a(0, 1, al);
+    rd_b(0, 0, bh);
+    rd_a(0, 0, ah);
+    rd_b(0, 1, bl);
+    for (int k = 0; k < KT; ++k) {
+      const bool more = k + 1 < KT;
+      pass(al, bh);
+      if (more) {
+        barrier_k(k + SB - 1 >= KT);   // B(k+1) and its chunk's window landed; reads of k retired
+        issue_at(k + 1);
+        rd_a(k + 1, 1, al);
+      }
+      pass(ah, bh);
+      if (more) rd_b(k + 1, 0, bh);
+      pass(ah, bl);
+      if (more) {
+        rd_a(k + 1, 0, ah);
+        rd_b(k + 1, 1, bl);
+      }
+    }
   }
   __syncthreads();
   stamp16(p.stamps, 2);
@@ -1173,10 +1254,13 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     return m < Mtot - HP && yy >= 0 && yy < HP - 2 && xx >= 0 && xx < HP - 2;
   };
   if constexpr (!FINAL) {
-    // bias + ReLU, bf16, 16-byte row stores through the LDS tile (two 128-column halves)
+    // bias + ReLU through the LDS tile (two 128-column halves): bf16 16-byte
+    // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
+    // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
     float* tile = reinterpret_cast<float*>(lds);
     constexpr int P4 = 128 + 4, C4 = 32, RS = NT / C4, IT = BMH / RS;
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
+    float mx[2] = {0.f, 0.f};   // SPLIT: max|out| of the tile's two ROIs (>= 0 after ReLU)
 #pragma unroll
     for (int h = 0; h < BN / 128; ++h) {
       if (h) __syncthreads();
@@ -1190,9 +1274,41 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
         int r, yy, xx;
         if (!interior(m, r, yy, xx)) continue;
         float4 x = *reinterpret_cast<const float4*>(tile + row * P4 + c4 * 4);
-        x.x = fmaxf(x.x + b.x, 0.f); x.y = fmaxf(x.y + b.y, 0.f);
-        x.z = fmaxf(x.z + b.z, 0.f); x.w = fmaxf(x.w + b.w, 0.f);
-        store4<__bf16>(out + (size_t)m * p.cout + co, x);
+        if constexpr (SPLIT) {
+          const int q = m >= rbound;
+          const float u = q ? us[1] : us[0], sc = q ? os[1] : os[0];
+          x.x = fmaxf(fmaf(x.x, u, b.x), 0.f); x.y = fmaxf(fmaf(x.y, u, b.y), 0.f);
+          x.z = fmaxf(fmaf(x.z, u, b.z), 0.f); x.w = fmaxf(fmaf(x.w, u, b.w), 0.f);
+          const float xv[4] = {x.x, x.y, x.z, x.w};
+          f16x4 hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xs = xv[e] * sc;
+            hi[e] = (_Float16)xs;
+            lo[e] = (_Float16)(xs - (float)hi[e]);
+          }
+          char* ob = static_cast<char*>(p.out) + (size_t)m * (p.cout * 4) + (co >> 5) * 128 + (co & 31) * 2;
+          *reinterpret_cast<f16x4*>(ob) = hi;
+          *reinterpret_cast<f16x4*>(ob + 64) = lo;
+          const float mc = fmaxf(fmaxf(x.x, x.y), fmaxf(x.z, x.w));
+          if (q) mx[1] = fmaxf(mx[1], mc); else mx[0] = fmaxf(mx[0], mc);
+        } else {
+          x.x = fmaxf(x.x + b.x, 0.f); x.y = fmaxf(x.y + b.y, 0.f);
+          x.z = fmaxf(x.z + b.z, 0.f); x.w = fmaxf(x.w + b.w, 0.f);
+          store4<__bf16>(out + (size_t)m * p.cout + co, x);
+        }
+      }
+    }
+    if constexpr (SPLIT) {
+      if (p.amax_idx >= 0) {   // per-ROI max|out| for the next conv's output scale
+        const float w0 = wave_max(mx[0]), w1 = wave_max(mx[1]);
+        if (lane == 0) {
+          if (w0 > 0.f)
+            atomicMax(reinterpret_cast<unsigned*>(p.hsc + (size_t)(p.r0 + rlo) * 4 + p.amax_idx), __float_as_uint(w0));
+          if (w1 > 0.f && rlo + 1 < p.R)
+            atomicMax(reinterpret_cast<unsigned*>(p.hsc + (size_t)(p.r0 + rlo + 1) * 4 + p.amax_idx),
+                      __float_as_uint(w1));
+        }
       }
     }
   } else {
@@ -1213,7 +1329,14 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaxf(acc[i][j][e] + bj, 0.f);
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (SPLIT) {
+            const float u = m0 + wm * WM + i * 16 + g * 4 + e >= rbound ? us[1] : us[0];
+            acc[i][j][e] = fmaxf(fmaf(acc[i][j][e], u, bj), 0.f);
+          } else {
+            acc[i][j][e] = fmaxf(acc[i][j][e] + bj, 0.f);
+          }
+        }
         v[i][j] = acc[i][j];
         quad_transpose(v[i][j], t4);
       }
@@ -1319,12 +1442,15 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
 
 hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
   if (a0.R <= 0) return hipSuccess;
-  const bool fin = a0.fin_w != nullptr;
-  if (a0.cin % 64 || (fin ? a0.cout != 64 : a0.cout % 128) || (fin && (!a0.slot || !a0.heat || !a0.fin_b)) ||
-      (!fin && !a0.out))
+  const bool fin = a0.fin_w != nullptr, split = a0.split != 0;
+  if (a0.cin % (split ? 32 : 64) || (fin ? a0.cout != 64 : a0.cout % 128) ||
+      (fin && (!a0.slot || !a0.heat || !a0.fin_b)) || (!fin && !a0.out) ||
+      (split && (!a0.hsc || a0.in_idx < 0 || a0.in_idx > 3 || a0.amax_idx > 3 || a0.out_idx > 3 ||
+                 (!fin && a0.out_idx < 0))))
     return hipErrorInvalidValue;
   HmConvArgs a = a0;
-  const long wt_bytes = (long)a.cout * 9 * a.cin * 2, roi_bytes = (long)HPP * a.cin * 2;
+  const long es = split ? 4 : 2;   // bytes per channel: bf16, or f16 hi + lo
+  const long wt_bytes = (long)a.cout * 9 * a.cin * es, roi_bytes = (long)HPP * a.cin * es;
   if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
   a.wt_bytes = (int)wt_bytes;
   const int chunk = (int)std::min<long>(a0.R, kMaxDesc / roi_bytes);
@@ -1333,7 +1459,7 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     a.R = nr;
     a.r0 = a0.r0 + r0;
     a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
-    if (!fin) a.out = static_cast<__bf16*>(a0.out) + (size_t)r0 * HPP * a.cout;
+    if (!fin) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.cout * es;
     a.in_bytes = (int)(nr * roi_bytes);
     const long rows = (long)nr * HPP - 2 * HP;
     // BN 256 with a 2-stage weight ring measured faster than BN 128 with 4
@@ -1355,7 +1481,12 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     const int bm = fin || bn != 256 ? BM : bm_env == 224 || bm_env == BM ? bm_env : (cost(224) < cost(BM) ? 224 : BM);
     const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
-    if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
+    if (split) {
+      if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true>), grid, dim3(NT), 0, st, a);
+      else if (bn == 256 && bm == 224) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true>), grid, dim3(NT), 0, st, a);
+      else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, BM, true>), grid, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((hmconv_kernel<128, 4, 0, BM, true>), grid, dim3(NT), 0, st, a);
+    } else if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && bm == 224 && dbg == 0) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 1) hipLaunchKernelGGL((hmconv_kernel<256, 2, 1>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 2) hipLaunchKernelGGL((hmconv_kernel<256, 2, 2>), grid, dim3(NT), 0, st, a);

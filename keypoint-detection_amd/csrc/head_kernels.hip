@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
 __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__ roi_stats,
                                                        const float* __restrict__ w0, const float* __restrict__ b0,
                                                        const float* __restrict__ w2, const float* __restrict__ b2,
-                                                       float* __restrict__ cw) {
+                                                       float* __restrict__ cw, float* __restrict__ hsc) {
   __shared__ float avg[TOPK], mx[TOPK], h[8];
   const int r = blockIdx.x, c = threadIdx.x;
   const float* st = roi_stats + (size_t)r * HM * 2 * TOPK;
@@ -265,6 +265,13 @@ __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__
   }
   avg[c] = s / (float)HMP;
   mx[c] = m;
+  if (hsc) {   // split heatmap convs: U0 = max of the ROI features bounds |xs| (sigmoid gates <= 1)
+    const float u0 = wave_max(m);
+    if (c == 0) {
+      hsc[(size_t)r * 4] = fmaxf(u0, 0.f);
+      hsc[(size_t)r * 4 + 1] = 0.f;   // max|h1|, published by heatmap conv 1
+    }
+  }
   __syncthreads();
   if (c < 8) {
     const int j = c & 3;
@@ -324,12 +331,13 @@ __global__ __launch_bounds__(64) void hm_spool_kernel(const float* __restrict__ 
 // pixel (lane x < 56, LDS), then xs = (roi * cw) * sw with lane (p, c) on
 // channels 4c .. 4c+3 of pixel 4i + p (1 KiB contiguous per load, the roi row
 // loads issued first), stored as the first heatmap conv's operand: bf16
-// zero-bordered [R][58][58][64] (out_bf16 == 2), bf16 [R][3136][64] (1) or
-// f32 (0).
+// zero-bordered [R][58][58][64] (out_bf16 == 2), bf16 [R][3136][64] (1),
+// f32 (0), or (3) zero-bordered f16 hi | lo of xs * 2^a0(r), 32-channel
+// [hi32 | lo32] groups, a0 = split_exp_of(hsc[r][0]) (split heatmap convs).
 __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
                                                        const float* __restrict__ smap, const float* __restrict__ saw,
                                                        const float* __restrict__ sab, void* __restrict__ xs,
-                                                       int out_bf16) {
+                                                       int out_bf16, const float* __restrict__ hsc) {
   constexpr int NI = HM / 4;
   __shared__ float w[98];
   __shared__ float2 srow[7][HM + 6];   // the 7 smap rows around y, zero-padded by 3 columns
@@ -377,13 +385,26 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
     ssw[x] = kpd_sigmoid(a + sab[0]);
   }
   const float4 cq = reinterpret_cast<const float4*>(cw + (size_t)r * TOPK)[c];
+  const float ssc = out_bf16 == 3 ? ldexpf(1.f, split_exp_of(hsc[(size_t)r * 4])) : 1.f;
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int px = 4 * i + pp;
     const float sw = ssw[px];
     const float4 o = make_float4((v[i].x * cq.x) * sw, (v[i].y * cq.y) * sw, (v[i].z * cq.z) * sw, (v[i].w * cq.w) * sw);
-    if (out_bf16) {
+    if (out_bf16 == 3) {
+      const size_t opix = ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1;
+      const float ov[4] = {o.x * ssc, o.y * ssc, o.z * ssc, o.w * ssc};
+      f16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (_Float16)ov[e];
+        lo[e] = (_Float16)(ov[e] - (float)hi[e]);
+      }
+      _Float16* ob = reinterpret_cast<_Float16*>(xs) + opix * 2 * TOPK + (c >> 3) * 64 + (c & 7) * 4;
+      *reinterpret_cast<f16x4*>(ob) = hi;
+      *reinterpret_cast<f16x4*>(ob + 32) = lo;
+    } else if (out_bf16) {
       const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1
                                         : ((size_t)r * HM + y) * HM + px;
       bf16x4 ob;
@@ -528,8 +549,8 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
   return hipGetLastError();
 }
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,
-                            const float* b2, float* cw, hipStream_t st) {
-  hipLaunchKernelGGL(hm_chattn_kernel, dim3(R), dim3(64), 0, st, roi_stats, w0, b0, w2, b2, cw);
+                            const float* b2, float* cw, float* hsc, hipStream_t st) {
+  hipLaunchKernelGGL(hm_chattn_kernel, dim3(R), dim3(64), 0, st, roi_stats, w0, b0, w2, b2, cw, hsc);
   return hipGetLastError();
 }
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st) {
@@ -537,8 +558,8 @@ hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap
   return hipGetLastError();
 }
 hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
-                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st) {
-  hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16);
+                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st, const float* hsc) {
+  hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16, hsc);
   return hipGetLastError();
 }
 hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot, int P,

@@ -60,11 +60,21 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
 // padded layout (interior only); else cout == 64 and the final 1x1 + sigmoid
 // is fused, writing heat [B][P][17][56][56] at the ROI's slot.
 struct HmConvArgs {
-  const void* in;        // [R][58][58][cin] bf16
-  const void* wt;        // [cout][9][cin] bf16 (BN folded)
+  const void* in;        // [R][58][58][cin] bf16, or (split) f16 [hi32 | lo32] per 32 channels
+  const void* wt;        // [cout][9][cin] bf16 (BN folded), or (split) f16 [hi32 | lo32] scaled 2^w_exp
   const float* bias;     // [cout]
-  void* out;             // [R][58][58][cout] bf16
+  void* out;             // [R][58][58][cout] bf16, or (split) f16 [hi32 | lo32]
   int R, cin, cout;
+  // split (fp32-accurate) mode: per-ROI bounds hsc[r][4]; the operand scale of
+  // ROI r is 2^a with a = split_exp_of(c + s * hsc[r][idx]) (kpd_common.h)
+  int split;
+  float* hsc;
+  float in_c, in_s;      // input bound
+  int in_idx;
+  float out_c, out_s;    // output bound (out_idx < 0: fp32 epilogue, conv 3)
+  int out_idx;
+  int amax_idx;          // >= 0: atomicMax of max|out| per ROI into hsc[r][amax_idx]
+  int w_exp;
   const float *fin_w, *fin_b;   // [17][64], [17]
   const int32_t* slot;
   int P;
@@ -203,11 +213,14 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
                             const float* boxes, int R, int P, float* roi, float* roi_stats,
                             hipStream_t st);
+// hsc != null (split heatmap convs): writes hsc[r][0] = max of ROI r's
+// features (the bound of |xs|) and zeroes hsc[r][1]
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0,
-                            const float* w2, const float* b2, float* cw, hipStream_t st);
+                            const float* w2, const float* b2, float* cw, float* hsc, hipStream_t st);
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st);
 hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
-                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st);
+                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st,
+                            const float* hsc = nullptr);
 hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot,
                            int P, float* heat_out, hipStream_t st);
 hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_t* slot, int R, int P,

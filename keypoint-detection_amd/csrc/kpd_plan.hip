@@ -84,6 +84,11 @@ struct DevConv {
   bool bf16 = false;
   void* w = nullptr;
   float* b = nullptr;
+  // split (fp32-accurate) copy for the heatmap-head convs: f16 [cout][9][cin/32][hi32 | lo32]
+  // of w * 2^w_exp, and the output bound |y| <= bc + bs * max|x| (bc = max|b|, bs = max_co sum|w|)
+  void* ws = nullptr;
+  int w_exp = 0;
+  float bc = 0.f, bs = 0.f;
 };
 struct DevDW { int C = 0, Cp = 0, k = 3, s = 1, act = 0; float* w = nullptr; float* b = nullptr; };
 struct DevSE { int C = 0, Cp = 0, sq = 0; float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr; };
@@ -111,6 +116,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* roi = nullptr;
   float* roi_stats = nullptr;
   float* cw = nullptr;
+  float* hsc = nullptr;   // split heatmap convs: per-ROI bounds [R][4] (max|xs|, max|h1|)
   float* smap = nullptr;
   void* xs = nullptr;
   void* h1 = nullptr;
@@ -342,6 +348,51 @@ int pack_plain(kpd_plan* p, const std::string& name, float** out, std::string& m
   return upload(p, w->data, out);
 }
 
+// Split (fp32-accurate) weights of a heatmap-head 3x3 conv (hmconv_kernel
+// SPLIT): the packed fp32 weights [cout_p][9][cin_p] scaled by 2^w_exp so
+// max|w| < 2^15, each value as f16 hi + lo, stored per 32 input channels as
+// [hi32 | lo32] (one 128-byte K-step row).  Also the output bound constants:
+// |y_co| <= |b_co| + sum|w_co| * max|x| <= bc + bs * max|x| (rounded up).
+int pack_split_hm(kpd_plan* p, DevConv& dc) {
+  const int cin = dc.cin_p, kk = dc.k * dc.k;
+  if (cin % 32 != 0) return fail(KPD_EINVAL, "split heatmap conv needs cin % 32 == 0");
+  const size_t n = (size_t)dc.cout_p * kk * cin;
+  std::vector<float> w(n), b(dc.cout_p);
+  HIP_TRY(hipMemcpy(w.data(), dc.w, n * sizeof(float), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(b.data(), dc.b, b.size() * sizeof(float), hipMemcpyDeviceToHost));
+  float mx = 0.f;
+  double bs = 0.0, bc = 0.0;
+  for (int co = 0; co < dc.cout_p; ++co) {
+    double sa = 0.0;
+    for (size_t i = 0; i < (size_t)kk * cin; ++i) {
+      const float v = w[(size_t)co * kk * cin + i];
+      mx = std::max(mx, std::fabs(v));
+      sa += std::fabs((double)v);
+    }
+    bs = std::max(bs, sa);
+    bc = std::max(bc, std::fabs((double)b[co]));
+  }
+  int e = 0;
+  if (mx > 0.f) std::frexp(mx, &e);
+  const int w_exp = std::min(std::max(14 - e, -100), 100);
+  std::vector<_Float16> hl(2 * n);
+  for (size_t row = 0; row < (size_t)dc.cout_p * kk; ++row)
+    for (int ci = 0; ci < cin; ++ci) {
+      const float x = std::ldexp(w[row * cin + ci], w_exp);
+      const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+      const size_t o = row * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
+      hl[o] = hi;
+      hl[o + 32] = lo;
+    }
+  _Float16* d = nullptr;
+  if (int rc = upload(p, hl, &d)) return rc;
+  dc.ws = d;
+  dc.w_exp = w_exp;
+  dc.bc = std::nextafter((float)(bc * (1.0 + 1e-6)), INFINITY);
+  dc.bs = std::nextafter((float)(bs * (1.0 + 1e-6)), INFINITY);
+  return KPD_OK;
+}
+
 // FPN level 0 by linearity (fpn0x_kernel): W0 = W3 . L0 (the 3x3 conv on the
 // 16-channel stem tap through the bias-free lateral 0) and, per output position
 // class (y % 4, x % 4), the 3x3 taps summed by the lateral-1 pixel they read
@@ -461,7 +512,7 @@ struct Carver {
 // (hmconv_kernel); KPD_NO_HMCONV=1 keeps the unpadded generic conv (A/B)
 bool hm_padded(const kpd_plan* p) {
   static const bool off = getenv("KPD_NO_HMCONV") != nullptr;
-  return p->precision == KPD_PRECISION_MIXED && !off;
+  return (p->precision == KPD_PRECISION_MIXED || p->precision == KPD_PRECISION_SPLIT) && !off;
 }
 
 size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
@@ -490,11 +541,12 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.scores = c.take<float>((size_t)B * 128);
   if (R > 0) {
     const size_t px = R * 3136;
-    const size_t es = p->precision == KPD_PRECISION_MIXED ? 2 : 4;
+    const size_t es = p->precision == KPD_PRECISION_MIXED ? 2 : 4;   // bf16, or f16 hi + lo / fp32
     w.slot = c.take<int32_t>(R);
     w.roi = c.take<float>(px * 64);
     w.roi_stats = c.take<float>(R * 56 * 2 * 64);
     w.cw = c.take<float>(R * 64);
+    w.hsc = c.take<float>(R * 4);
     w.smap = c.take<float>(px * 2);
     // mixed: zero-bordered 58x58 ROI maps for the padded heatmap convs (hmconv_kernel)
     const size_t pxp = hm_padded(p) ? R * kHmPad * kHmPad : px;
@@ -597,8 +649,29 @@ int conv(const DevConv& L, const void* in, int N, int H, int W, int in_cstride, 
 // fin (bf16 path, out_kind 2 only): fuse the final 1x1 + sigmoid into the
 // epilogue and write the heatmap instead of `out` (conv_glds.hip).
 struct HmFinal { const float *w, *b; const int32_t* slot; int P; float* heat; };
+// split mode: per-ROI operand bounds (HmConvArgs) -- input u_in = in_c + in_s *
+// hsc[r][in_idx], output u_out = out_c + out_s * hsc[r][out_idx], max|out|
+// published into hsc[r][amax_idx]
+struct HmSplit { float* hsc; float in_c, in_s; int in_idx; float out_c, out_s; int out_idx, amax_idx; };
 int hm_conv(const kpd_plan* p, const DevConv& L, const void* in, int R, int in_cstride, void* out, int out_kind,
-            hipStream_t st, const HmFinal* fin = nullptr, unsigned long long* stamps = nullptr) {
+            hipStream_t st, const HmFinal* fin = nullptr, unsigned long long* stamps = nullptr,
+            const HmSplit* sp = nullptr) {
+  if (L.ws) {   // fp32-accurate split products on the padded ROI maps
+    if (!sp || !hm_padded(p)) return fail(KPD_EINVAL, "split heatmap conv needs the padded layout and bounds");
+    HmConvArgs h{};
+    h.in = in; h.wt = L.ws; h.bias = L.b; h.out = out; h.R = R; h.cin = L.cin_p; h.cout = L.cout_p;
+    h.stamps = stamps;
+    h.split = 1; h.hsc = sp->hsc; h.w_exp = L.w_exp;
+    h.in_c = sp->in_c; h.in_s = sp->in_s; h.in_idx = sp->in_idx;
+    h.out_c = sp->out_c; h.out_s = sp->out_s; h.out_idx = sp->out_idx; h.amax_idx = sp->amax_idx;
+    if (fin) {
+      if (L.cout_p != 64) return fail(KPD_EINVAL, "fused final layer needs the 64-channel conv");
+      h.fin_w = fin->w; h.fin_b = fin->b; h.slot = fin->slot; h.P = fin->P; h.heat = fin->heat;
+      h.out_idx = -1;
+    }
+    HIP_TRY(launch_hmconv(h, st));
+    return KPD_OK;
+  }
   if (!L.bf16) return conv(L, in, R, 56, 56, in_cstride, out, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
   if (hm_padded(p)) {
     if (in_cstride != L.cin_p) return fail(KPD_EINVAL, "hmconv: input channel stride must equal cin");
@@ -678,7 +751,7 @@ void kpd_plan_destroy(kpd_plan* p) {
 
 int kpd_plan_finalize(kpd_plan* p, int precision) {
   if (!p) return fail(KPD_EINVAL, "null plan");
-  if (precision != KPD_PRECISION_FP32 && precision != KPD_PRECISION_MIXED)
+  if (precision != KPD_PRECISION_FP32 && precision != KPD_PRECISION_MIXED && precision != KPD_PRECISION_SPLIT)
     return fail(KPD_EINVAL, "unknown precision");
   HIP_TRY(hipSetDevice(p->device));
   for (void* a : p->allocs) (void)hipFree(a);
@@ -687,6 +760,9 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   p->stamps = nullptr;
   p->pd = DevConv();
   p->anchors = nullptr;
+  p->hm1 = DevConv();
+  p->hm2 = DevConv();
+  p->hm3 = DevConv();
   p->kh_ds1 = DevConv();
   p->kh_ds2 = DevConv();
   p->has_kh = false;
@@ -751,7 +827,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
-  if (precision == KPD_PRECISION_MIXED && rc == KPD_OK && missing.empty()) chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
+  if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty()) chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
@@ -770,6 +846,11 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
                 bf, p->hm2, missing));
   chk(pack_conv(p, Hh + "final_layer.0.weight", Hh + "final_layer.0.bias", Hh + "final_layer.1", 1e-5, 3, bf,
                 p->hm3, missing));
+  if (precision == KPD_PRECISION_SPLIT && rc == KPD_OK && missing.empty()) {
+    chk(pack_split_hm(p, p->hm1));
+    chk(pack_split_hm(p, p->hm2));
+    chk(pack_split_hm(p, p->hm3));
+  }
   chk(pack_plain(p, Hh + "final_layer.3.weight", &p->fin_w, missing, 17 * 64));
   chk(pack_plain(p, Hh + "final_layer.3.bias", &p->fin_b, missing, 17));
   {
@@ -866,7 +947,7 @@ static int max_pass_images(int H, int W) {
 // lateral 1 an exact 4x nearest upsample of the level-0 grid)
 static bool fpn0x_ok(const kpd_plan* p, const Dims& d) {
   static const bool no_lin = getenv("KPD_NO_FPN0X") != nullptr;   // A/B switch
-  return p->precision == KPD_PRECISION_MIXED && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] &&
+  return p->precision != KPD_PRECISION_FP32 && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] &&
          d.Wf == 4 * d.w[3] && (long)((d.h[3] * d.w[3] + 255) / 256) * 256 < 65536;
 }
 
@@ -1162,26 +1243,35 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   }
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
   std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
-  HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw, st));
+  // split: per-ROI operand bounds, hsc[r] = {max|xs| (written here), max|h1| (conv 1)}
+  const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
+  HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw,
+                           hsplit ? w.hsc : nullptr, st));
   HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
   const bool bf = p->precision == KPD_PRECISION_MIXED;
-  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, bf ? (hm_padded(p) ? 2 : 1) : 0, st));
+  const int xs_mode = hsplit ? 3 : bf ? (hm_padded(p) ? 2 : 1) : 0;
+  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc));
   att_stage.reset();
+  // bounds: |xs| <= U0; |h1| <= bc1 + bs1 U0; |h2| <= bc2 + bs2 max|h1| (the
+  // exponent each producer scales by and its consumer unscales by)
+  const HmSplit sp1{w.hsc, 0.f, 1.f, 0, p->hm1.bc, p->hm1.bs, 0, 1};
+  const HmSplit sp2{w.hsc, p->hm1.bc, p->hm1.bs, 0, p->hm2.bc, p->hm2.bs, 1, -1};
+  const HmSplit sp3{w.hsc, p->hm2.bc, p->hm2.bs, 1, 0.f, 0.f, -1, -1};
   std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
-  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st)) return rc;
+  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st, nullptr, nullptr, &sp1)) return rc;
   c1.reset();
   std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
   if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st, nullptr,
-                       take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
+                       take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2), &sp2))
     return rc;
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
-  // mixed: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
+  // mixed / split: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
   static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
-  const bool fin_fused = p->hm3.bf16 && p->hm3.cout_p == 64 && !no_fin_fuse;
+  const bool fin_fused = (p->hm3.bf16 || p->hm3.ws) && p->hm3.cout_p == 64 && (!no_fin_fuse || p->hm3.ws);
   const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
   if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr,
-                       take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
+                       take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2), &sp3))
     return rc;
   c3.reset();
   {

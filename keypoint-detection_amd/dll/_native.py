@@ -17,7 +17,12 @@ _lib: Optional[ctypes.CDLL] = None
 
 KPD_PRECISION_FP32 = 0
 KPD_PRECISION_MIXED = 1
-PRECISIONS = {"fp32": KPD_PRECISION_FP32, "mixed": KPD_PRECISION_MIXED, "bf16": KPD_PRECISION_MIXED}
+KPD_PRECISION_SPLIT = 2
+# "fp32": every conv on fp32-input MFMA; "split": fp32-accurate -- FPN level 0
+# and the heatmap-head convs as three f16 MFMA products of hi/lo operand
+# splits (fp32 tolerances); "mixed": split FPN level 0 + bf16 heatmap convs
+PRECISIONS = {"fp32": KPD_PRECISION_FP32, "split": KPD_PRECISION_SPLIT, "mixed": KPD_PRECISION_MIXED,
+              "bf16": KPD_PRECISION_MIXED}
 
 # every symbol include/kpd.h declares (checked by tests/test_abi.py)
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
