@@ -89,35 +89,182 @@ def parse():
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=192)
     ap.add_argument("--persons", type=int, default=1)
-    ap.add_argument("--precision", default="mixed", choices=["fp32", "split", "mixed"])
-    ap.add_argument("--cpu-sample", type=int, default=8, help="images in the CPU-baseline sample")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"],
+                    help="split = fp32-accurate (the reference's precision); mixed = bf16 heatmap convs")
+    ap.add_argument("--secondary", default="mixed", help="second, labelled precision line at N=1 ('' = none)")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="sub-batch streams inside one forward (kpd_plan_set_streams)")
-    ap.add_argument("--roof-iters", type=int, default=5,
-                    help="isolated single-stream forwards timed for the roofline kernel")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r01" / "pmc.json"),
+    ap.add_argument("--streams", type=int, default=1,
+                    help="sub-batch streams inside one forward (kpd_plan_set_streams); 2 overlaps the sub-batches "
+                         "(~4%% more images/s) but then every kernel shares the GPU and its launch time no longer "
+                         "describes the kernel")
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r02" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
 
 
-def cpu_baseline(sd, img, boxes, seconds, threads):
-    """The oracle (a plain-torch restatement of the reference forward, same
-    per-box loop) timed on this host's cores."""
+def host_cpu_info():
+    """CPU model, machine core counts and the CPU share this process may use
+    (cgroup v2 cpu.max quota / affinity), for the baseline's `cores`."""
+    info = {"model": None, "physical_cores": None, "logical_cpus": os.cpu_count(), "cgroup_cpus": None}
+    try:
+        phys, model = set(), None
+        with open("/proc/cpuinfo") as fh:
+            pid = cid = None
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    cid = v
+                elif not k and pid is not None:
+                    phys.add((pid, cid))
+                    pid = cid = None
+        info["model"], info["physical_cores"] = model, len(phys) or None
+    except OSError:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_cpus"] = int(q) // int(per)
+    except (OSError, ValueError):
+        pass
+    avail = [len(os.sched_getaffinity(0))]
+    if info["cgroup_cpus"]:
+        avail.append(info["cgroup_cpus"])
+    if info["physical_cores"]:
+        avail.append(info["physical_cores"])
+    info["threads"] = max(1, min(avail))
+    return info
+
+
+def cpu_baseline(sd, img, boxes, threads, warmups=3, runs=5, max_seconds=40.0):
+    """The oracle (a plain-torch restatement of the reference forward with its
+    per-box loop, golden-pinned) timed on this host: `warmups` untimed runs,
+    then the median of `runs` timed runs of the whole sample (fewer if one run
+    would push the total past max_seconds)."""
     from oracle import kpd_oracle as O
     torch.set_num_threads(threads)
     batch = {"image": img, "bboxes": boxes}
-    out = O.forward(sd, batch)        # warmup + outputs for parity
-    runs, t0 = 0, time.perf_counter()
-    while True:
+    t0 = time.perf_counter()
+    out = O.forward(sd, batch)        # first warmup: also the parity outputs
+    once = time.perf_counter() - t0
+    warmups = max(1, min(warmups, int(max_seconds / 3 / max(once, 1e-3))))
+    for _ in range(warmups - 1):
         O.forward(sd, batch)
-        runs += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or runs >= 50:
-            break
-    return out, img.shape[0] * runs / el, runs
+    runs = max(5, min(runs, int(max_seconds / max(once, 1e-3))))
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        O.forward(sd, batch)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    return out, img.shape[0] / med, {"warmups": warmups, "runs": runs, "median_s": round(med, 4),
+                                     "min_s": round(ts[0], 4), "max_s": round(ts[-1], 4)}
+
+
+def run_steps(m, batch, steps, warmup, step_fn, dist):
+    """W untimed + K timed steps bracketed by barrier + synchronize; seconds."""
+    import torch.distributed as tdist
+    with torch.no_grad():
+        for _ in range(warmup):
+            step_fn()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step_fn()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        return time.perf_counter() - t0, out
+
+
+def stage_pass(m, plan, batch, iters):
+    """Per-stage HIP-event means (events on each sub-batch's launch stream) of
+    `iters` forwards in the run's own configuration (same sub-batch streams,
+    so every kernel launch has the shape the timed region launches)."""
+    from dll import _native
+    with torch.no_grad():
+        torch.cuda.synchronize()
+        plan.timing(True)
+        for _ in range(iters):
+            m(batch)
+        torch.cuda.synchronize()
+        plan.timing(False)
+    st = {}
+    for s in _native.STAGES:
+        ms, n = plan.timing_query(s)
+        if n:
+            st[s] = (ms / n, n)
+    return st
+
+
+def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
+    """Roofline of the dominant kernel (the longest single-kernel MFMA stage).
+    achieved = ALGORITHMIC flops per launch (SURVEY §8(d)) / mean launch time;
+    peak = dense MFMA peak of the dtype the kernel issues (f16/bf16 2.5 PF,
+    f32 157.3 TF).  The MFMA work actually issued (split products, padded
+    border rows, FPN level 0 by linearity) is reported beside it."""
+    hf, wf = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    h1, w1 = hf, wf
+    for _cin, k, _e, _co, _se, _a, st in BNECK[:3]:
+        pd = (k - 1) // 2
+        h1, w1 = (h1 + 2 * pd - k) // st + 1, (w1 + 2 * pd - k) // st + 1
+    split_fpn = precision in ("split", "mixed") and hf == 4 * h1 and wf == 4 * w1
+    pad = 58 * 58 / (56 * 56)    # hmconv computes the padded ROI rows (border rows discarded)
+    kern = {}
+    if split_fpn:
+        ex = 3 * 2.0 * hf * wf * (5 * 32 * 128 + 36 * 128 * 128 / 16) * B
+        kern["fpn0"] = (fl["fpn0"] * B, PEAK_TFLOPS["bf16"], ex, "fpn0x_kernel",
+                        "FPN level-0 conv3x3 128->128 by linearity (composite 16-ch 3x3 on the stem tap + per-"
+                        "position-class lateral-1 tap groups), fp32-accurate: 3 f16 products per MAC on "
+                        "v_mfma_f32_16x16x32_f16")
+    else:
+        kern["fpn0"] = (fl["fpn0"] * B, PEAK_TFLOPS["fp32"], fl["fpn0"] * B, "conv_mfma_kernel",
+                        "FPN level-0 conv3x3 on v_mfma_f32_16x16x4_f32")
+    for s in ("hm_conv1", "hm_conv2", "hm_conv3"):
+        f = fl[s] * B
+        if precision == "split":
+            kern[s] = (f, PEAK_TFLOPS["bf16"], 3 * f * pad, "hmconv_kernel<SPLIT>",
+                       f"{s} conv3x3 on zero-bordered ROI maps, fp32-accurate: 3 f16 products per MAC on "
+                       "v_mfma_f32_16x16x32_f16")
+        elif precision == "mixed":
+            kern[s] = (f, PEAK_TFLOPS["bf16"], f * pad, "hmconv_kernel",
+                       f"{s} conv3x3 on zero-bordered ROI maps, bf16 operands on v_mfma_f32_16x16x32_bf16")
+        else:
+            kern[s] = (f, PEAK_TFLOPS["fp32"], f, "conv_mfma_kernel", f"{s} conv3x3 on v_mfma_f32_16x16x4_f32")
+    cand = [s for s in kern if s in stages]
+    if not cand:
+        return None
+    if dom is None:
+        dom = max(cand, key=lambda k: stages[k])
+    flop, peak, exflop, kname, desc = kern[dom]
+    t = stages[dom] * 1e-3
+    ach, exa = flop / t / 1e12, exflop / t / 1e12
+    r = {"bound": "mfma", "kernel": kname, "desc": desc, "stage": dom, "achieved": round(ach, 2), "peak": peak,
+         "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+         "flop_per_launch": flop, "avg_ms": round(stages[dom], 4),
+         "executed_flop_per_launch": exflop, "executed_achieved": round(exa, 2),
+         "executed_frac": round(exa / peak, 4)}
+    if exflop > 2.5 * flop:   # 3-product split: each fp32 MAC costs 3 MFMA products
+        r["split_ceiling_frac"] = round(ach / (peak / 3.0), 4)
+    e = pmc.get(f"{dom}:{precision}") if pmc else None
+    if e:
+        r["traffic"] = e.get("hbm_bytes_per_launch")
+        r["traffic_unit"] = "HBM bytes/launch: rocprofv3 --pmc, 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)"
+        if e.get("SQ_VALU_MFMA_BUSY_CYCLES") and e.get("GRBM_GUI_ACTIVE"):
+            # MFMA-busy cycles summed over the 1024 SIMDs / (GUI-active cycles per XCD)
+            r["mfma_busy_frac"] = round(e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"]), 4)
+        r["pmc_source"] = e.get("source")
+    return r
 
 
 def main():
@@ -132,15 +279,17 @@ def main():
         import torch.distributed as tdist
         tdist.init_process_group("nccl", device_id=dev)
 
-    from dll import _native
     from dll.configs import ModelConfig, TrainingConfig
     from dll.models import MultiPersonKeypointModel
     from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
 
-    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=a.precision, streams=a.streams)
-    sd = synthetic_state_dict(m.state_dict(), seed=0)
-    m.load_state_dict(sd)
-    m = m.to(dev).eval()
+    def build(precision):
+        m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=precision, streams=a.streams)
+        m.load_state_dict(sd)
+        return m.to(dev).eval()
+
+    sd = synthetic_state_dict(MultiPersonKeypointModel(ModelConfig(), TrainingConfig()).state_dict(), seed=0)
+    m = build(a.precision)
     B, P = a.batch, a.persons
     img_cpu = synthetic_images(B, 3, a.height, a.width, seed=1234 + 7919 * rank)
     box_cpu = synthetic_boxes(B, P, seed=1235 + 7919 * rank)
@@ -152,113 +301,63 @@ def main():
     if gather:
         from dll.distributed import collate_outputs
 
-    def step():
-        out = m(batch)
-        if gather:   # result collation over RCCL: P all_reduce(MAX) + kpt/vis all_gather
+    def step(model=m):
+        out = model(batch)
+        if gather:   # result collation over RCCL: all_gather of the kpt / vis slabs (P known: no host sync)
             collate_outputs(out, B * world, max_persons=P)
         return out
 
+    n_sub = max(1, min(a.streams, 4, B // 16))
+    Bl = B // n_sub if B % n_sub == 0 else B / n_sub      # images per kernel launch (one sub-batch)
+    # warm-up, then one forward with every stage's events (the breakdown), then
+    # the timed region with events around the dominant MFMA kernel only (no
+    # bubbles elsewhere): its mean launch time is the roofline's denominator
     with torch.no_grad():
         for _ in range(a.warmup):
-            out = step()
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        # no per-stage events in the timed region: each hipEventRecord between
-        # stages costs a ~10 us bubble on the queue
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            out = step()
-        torch.cuda.synchronize()
-        if dist:
-            tdist.barrier()
-        el = time.perf_counter() - t0
-        # Roofline pass: with sub-batch streams every kernel shares the GPU with
-        # the other sub-batch, so its launch duration in the timed region does
-        # not describe the kernel.  Re-time it in a few single-stream forwards
-        # (same inputs, HIP events on the launch stream).
-        plan.set_streams(1)
-        torch.cuda.synchronize()
-        plan.timing(True)
-        for _ in range(a.roof_iters):
-            m(batch)
-        torch.cuda.synchronize()
-        plan.timing(False)
-        plan.set_streams(a.streams)
+            step()
+    breakdown = stage_pass(m, plan, batch, 1)
+    mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
+    dom = max((k for k in breakdown if k in mfma_stages), key=lambda k: breakdown[k][0], default=None)
+    plan.timing(True, stage=dom)
+    el, out = run_steps(m, batch, a.steps, 0, step, dist)
+    plan.timing(False)
+    dms, dn = plan.timing_query(dom) if dom else (0.0, 0)
+    stages = {k: v[0] for k, v in breakdown.items()}
+    if dn:
+        stages[dom] = dms / dn
     el_t = torch.tensor([el], device=dev, dtype=torch.float64)
     if dist:
         tdist.all_reduce(el_t, op=tdist.ReduceOp.MAX)
     el = float(el_t.item())
 
-    stages = {}
-    for s in _native.STAGES:
-        ms, n = plan.timing_query(s)
-        if n:
-            stages[s] = ms / n
     fl = flops_per_image(a.height, a.width, P)
-    mixed = a.precision == "mixed"
-    # stage records of the roofline pass are whole-batch (single-stream) launches
-    n_sub = max(1, min(a.streams, 4, B // 16))
-    Bl = B
-    # (label, peak TFLOP/s for the ALGORITHMIC flops, kernel description)
-    # mixed precision with an exact 4x lateral-1 upsample runs FPN level 0 by
-    # linearity (fpn0x_kernel): the ALGORITHMIC flops stay those of the 3x3
-    # conv over lateral 0; the MFMA work actually issued is
-    # reported beside them (executed_*)
-    hf, wf = (a.height - 1) // 2 + 1, (a.width - 1) // 2 + 1
-    h1, w1 = hf, wf
-    for _cin, k, _e, _co, _se, _a, st in BNECK[:3]:
-        pd = (k - 1) // 2
-        h1, w1 = (h1 + 2 * pd - k) // st + 1, (w1 + 2 * pd - k) // st + 1
-    lin = mixed and hf == 4 * h1 and wf == 4 * w1
-    exec_fpn0 = (2.0 * hf * wf * (5 * 32 * 128 + 36 * 128 * 128 / 16) * Bl) if lin else None
-    mfma = {"fpn0": (fl["fpn0"] * Bl, PEAK_TFLOPS["bf16"] / 3.0 if mixed else PEAK_TFLOPS["fp32"],
-                     ("fpn0 conv3x3 128->128 by linearity (composite 16-ch 3x3 on the stem tap + per-position-class "
-                      "lateral-1 tap groups), fp32-accurate 3-product f16 split on v_mfma_f32_16x16x32_f16 "
-                      "(peak = 2500/3 TF/s fp32-equivalent)") if lin else
-                     "fpn0 conv3x3 128->128: fp32-accurate 3-product f16 split on v_mfma_f32_16x16x32_f16 "
-                     "(peak = 2500/3 TF/s fp32-equivalent)" if mixed else
-                     "fpn0 conv3x3 128->128 on v_mfma_f32_16x16x4_f32")}
-    for s in ("hm_conv1", "hm_conv2", "hm_conv3"):
-        mfma[s] = (fl[s] * Bl, PEAK_TFLOPS["bf16" if mixed else "fp32"],
-                   f"{s} implicit-GEMM conv3x3 ({'bf16' if mixed else 'fp32'} MFMA)")
-    # dominant KERNEL: the longest single-kernel MFMA stage ("body" is ~50 small launches)
-    cand = [s for s in mfma if s in stages]
-    dom = max(cand, key=lambda k: stages[k]) if cand else None
-    roof = None
-    if dom in mfma:
-        flop, peak, desc = mfma[dom]
-        ach = flop / (stages[dom] * 1e-3) / 1e12
-        traffic = None
-        pj = Path(a.pmc_json)
-        if pj.exists():
-            try:
-                traffic = json.loads(pj.read_text()).get(f"{dom}:{a.precision}", {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        roof = {"bound": "mfma", "kernel": desc, "stage": dom, "achieved": round(ach, 2), "peak": round(peak, 1),
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                "traffic_unit": "bytes/launch (rocprofv3 PMC, 2*FETCH_SIZE+WRITE_SIZE)",
-                "flop_per_launch": flop, "avg_ms": round(stages[dom], 4)}
-        if dom == "fpn0" and exec_fpn0:
-            ex = exec_fpn0 / (stages[dom] * 1e-3) / 1e12
-            roof.update({"executed_flop_per_launch": exec_fpn0, "executed_achieved": round(ex, 2),
-                         "executed_frac": round(ex / peak, 4)})
-
+    pmc = None
+    pj = Path(a.pmc_json)
+    if pj.exists():
+        try:
+            pmc = json.loads(pj.read_text())
+        except ValueError:
+            pmc = None
+    roof = roofline(a.precision, stages, fl, Bl, a.height, a.width, pmc, dom)
+    if roof:
+        roof["launches_timed"] = dn
+        roof["images_per_launch"] = Bl
+        roof["timing"] = ("HIP events around every launch of this kernel inside the timed region, on the "
+                          "sub-batch stream it is launched on")
     total_imgs = B * world * a.steps
+    dtypes = {"split": ("fp32", "fp32-accurate: body/laterals/heads fp32; FPN level 0 and the heatmap-head convs "
+                                "as 3 f16 MFMA products of hi/lo operand splits (fp32 tolerances), fp32 accumulate"),
+              "fp32": ("fp32", "every conv on fp32-input MFMA (exact fp32 products)"),
+              "mixed": ("bf16", "heatmap-head convs bf16 x bf16 (fp32 accumulate); backbone/FPN fp32-accurate")}
     line = {
         "metric": "images/sec @ 256x192 COCO-17 (MultiPersonKeypointModel.forward, given boxes)",
         "value": round(total_imgs / el, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        # mixed: body + laterals fp32, FPN level-0 conv fp32-accurate f16x3 split,
-        # heatmap-head convs bf16; every accumulation fp32
-        "dtype": "f32+f16x3+bf16" if a.precision == "mixed" else "f32",
+        "dtype": dtypes[a.precision][0], "dtype_detail": dtypes[a.precision][1],
         "data": "synthetic (seeded U[0,1) images ImageNet-normalised, seeded boxes, seed-0 random weights)",
-        "config": {"workload": "C2: batch 64/GPU, 256x192x3, 1 box/img, heatmap head + soft-argmax decode",
+        "config": {"workload": f"C2: batch {B}/GPU, {a.height}x{a.width}x3, {P} box/img, heatmap head + "
+                               "soft-argmax decode",
                    "model": "MultiPersonKeypointModel (MobileNetV3-Small+FPN, HeatmapHead)",
                    "global_batch": B * world, "height": a.height, "width": a.width, "persons": P,
                    "precision": a.precision, "parallelism": f"dp{world}", "streams_per_gpu": n_sub,
@@ -267,21 +366,51 @@ def main():
         "achieved_tflops_total": round(fl["total"] * total_imgs / el / 1e12, 2),
         "roofline": roof,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-        "roofline_pass": f"{a.roof_iters} single-stream forwards after the timed region",
+        "stages_note": f"per launch (one sub-batch of {Bl} images): one forward with every stage's HIP events "
+                       "before the timed region; the dominant stage's figure is its timed-region mean",
         "cpu_baseline": None,
     }
+    if world == 1 and a.secondary and a.secondary != a.precision:
+        # the same workload at the second precision (labelled; not the headline)
+        m2 = build(a.secondary)
+        p2 = m2.native_plan(dev)
+        with torch.no_grad():
+            for _ in range(a.warmup):
+                step(m2)
+        bd2 = stage_pass(m2, p2, batch, 1)
+        d2 = max((k for k in bd2 if k in mfma_stages), key=lambda k: bd2[k][0], default=None)
+        p2.timing(True, stage=d2)
+        el2, _ = run_steps(m2, batch, a.steps, 0, lambda: step(m2), False)
+        p2.timing(False)
+        st2 = {k: v[0] for k, v in bd2.items()}
+        if d2:
+            ms2, n2 = p2.timing_query(d2)
+            if n2:
+                st2[d2] = ms2 / n2
+        line["secondary"] = {"precision": a.secondary, "dtype": dtypes[a.secondary][0],
+                             "dtype_detail": dtypes[a.secondary][1], "value": round(B * a.steps / el2, 2),
+                             "ms_per_step": round(el2 / a.steps * 1e3, 4),
+                             "roofline": roofline(a.secondary, st2, fl, Bl, a.height, a.width, pmc, d2),
+                             "stages_ms": {k: round(v, 4) for k, v in st2.items()}}
+        del m2, p2
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        ci = host_cpu_info()
         S = min(a.cpu_sample, B)
-        ref, cpu_rate, runs = cpu_baseline(sd, img_cpu[:S], box_cpu[:S], a.cpu_seconds, threads)
-        line["cpu_baseline"] = {"value": round(cpu_rate, 3), "unit": "images/s", "cores": threads, "kind": "port",
-                                "sample": f"{S} images x {runs} runs of the same workload (oracle/kpd_oracle.py "
-                                          f"forward, per-box loop as the reference)"}
+        ref, cpu_rate, proto = cpu_baseline(sd, img_cpu[:S], box_cpu[:S], ci["threads"])
+        line["cpu_baseline"] = {
+            "value": round(cpu_rate, 3), "unit": "images/s", "cores": ci["threads"], "kind": "port",
+            "sample": f"{S} images of the same C2 workload, oracle/kpd_oracle.py forward (the reference's per-box "
+                      f"loop, golden-pinned), {proto['warmups']} warmups + median of {proto['runs']} runs",
+            "protocol": proto, "cpu_model": ci["model"], "machine_physical_cores": ci["physical_cores"],
+            "machine_logical_cpus": ci["logical_cpus"], "cgroup_cpu_quota": ci["cgroup_cpus"],
+            "threads_note": "torch threads = min(affinity, cgroup cpu.max quota, physical cores): the CPU share "
+                            "this job may use on the GPU box"}
         line["gpu_vs_cpu"] = round(line["value"] / cpu_rate, 1)
         gk = out["keypoints"][:S].cpu()
         d = (gk - ref["keypoints"]).norm(dim=-1)
         line["parity"] = {"pck@0.5": float((d <= 0.5).float().mean()), "pck@0.002": float((d <= 0.002).float().mean()),
                           "max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
+                          "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
                           "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
                           "images": S}
     if rank == 0:

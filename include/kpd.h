@@ -108,6 +108,10 @@ int kpd_debug_copy(kpd_plan* plan, const char* name, void* dst, size_t bytes, si
  * ("body", "fpn_lateral", "fpn0", "topk", "roi_align", "hm_attention",
  * "hm_conv1", "hm_conv2", "hm_conv3", "hm_final_decode"). */
 int kpd_plan_timing(kpd_plan* plan, int enable);
+/* Restrict the recording to one stage (NULL or "" = every stage): a single
+ * kernel timed inside a throughput run without the other stages' event
+ * bubbles. */
+int kpd_plan_timing_stage(kpd_plan* plan, const char* stage);
 int kpd_plan_timing_query(kpd_plan* plan, const char* stage, double* total_ms, int* count);
 
 /* Greedy NMS on one set of n cxcywh boxes (device), reference semantics

@@ -1020,7 +1020,10 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // DMA inside the K loop (the prologue's still lands)
 // BMH: GEMM rows per tile (256, or 224 so that the tile count packs the CUs'
 // rounds better -- launch_hmconv picks it; the window stays 384 rows)
-template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false>
+// CIN: input channels as a compile-time constant (0 = p.cin): the K loop's
+// trip count is then known to the compiler, and conv 1 / conv 2 are separate
+// kernels in a trace
+template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0>
 __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
@@ -1042,7 +1045,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   const int m0 = HP + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
   // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
   // channels as [hi32 | lo32] f16
-  const int Mtot = p.R * HPP, cin = p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = 9 * NC;
+  const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = 9 * NC;
   stamp16(p.stamps, 0);
   const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
@@ -1481,17 +1484,24 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     const int bm = fin || bn != 256 ? BM : bm_env == 224 || bm_env == BM ? bm_env : (cost(224) < cost(BM) ? 224 : BM);
     const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
+#define HMK(...) hipLaunchKernelGGL((hmconv_kernel<__VA_ARGS__>), grid, dim3(NT), 0, st, a)
     if (split) {
-      if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true>), grid, dim3(NT), 0, st, a);
-      else if (bn == 256 && bm == 224) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true>), grid, dim3(NT), 0, st, a);
-      else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, BM, true>), grid, dim3(NT), 0, st, a);
-      else hipLaunchKernelGGL((hmconv_kernel<128, 4, 0, BM, true>), grid, dim3(NT), 0, st, a);
+      if (fin && a.cin == 256) HMK(64, 4, 0, BM, true, 256);
+      else if (fin) HMK(64, 4, 0, BM, true);
+      else if (bn == 256 && bm == 224 && a.cin == 64) HMK(256, 2, 0, 224, true, 64);
+      else if (bn == 256 && bm == 224 && a.cin == 256) HMK(256, 2, 0, 224, true, 256);
+      else if (bn == 256 && bm == 224) HMK(256, 2, 0, 224, true);
+      else if (bn == 256) HMK(256, 2, 0, BM, true);
+      else HMK(128, 4, 0, BM, true);
     } else if (fin) hipLaunchKernelGGL((hmconv_kernel<64, 4>), grid, dim3(NT), 0, st, a);
+    else if (bn == 256 && bm == 224 && dbg == 0 && a.cin == 64) HMK(256, 2, 0, 224, false, 64);
+    else if (bn == 256 && bm == 224 && dbg == 0 && a.cin == 256) HMK(256, 2, 0, 224, false, 256);
     else if (bn == 256 && bm == 224 && dbg == 0) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 1) hipLaunchKernelGGL((hmconv_kernel<256, 2, 1>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 2) hipLaunchKernelGGL((hmconv_kernel<256, 2, 2>), grid, dim3(NT), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2>), grid, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((hmconv_kernel<128, 4>), grid, dim3(NT), 0, st, a);
+#undef HMK
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

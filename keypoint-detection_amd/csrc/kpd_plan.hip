@@ -208,6 +208,7 @@ struct kpd_plan {
   // per-stage HIP-event timing (kpd_plan_timing)
   struct Timer { std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; size_t used = 0; };
   bool timing = false;
+  std::string timing_only;   // non-empty: record only this stage (kpd_plan_timing_stage)
   std::map<std::string, Timer> timers;
 };
 
@@ -608,7 +609,7 @@ struct Stage {
   hipStream_t st;
   hipEvent_t end = nullptr;
   Stage(kpd_plan* plan, const char* name, hipStream_t stream) : p(plan), st(stream) {
-    if (!p->timing) return;
+    if (!p->timing || (!p->timing_only.empty() && p->timing_only != name)) return;
     auto& t = p->timers[name];
     if (t.used == t.ev.size()) {
       hipEvent_t a, b;
@@ -1416,6 +1417,12 @@ int kpd_plan_timing(kpd_plan* p, int enable) {
   p->timing = enable != 0;
   if (p->timing)
     for (auto& kv : p->timers) kv.second.used = 0;
+  return KPD_OK;
+}
+
+int kpd_plan_timing_stage(kpd_plan* p, const char* stage) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  p->timing_only = stage ? stage : "";
   return KPD_OK;
 }
 

@@ -27,7 +27,8 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "split": KPD_PRECISION_SPLIT, "mixed":
 # every symbol include/kpd.h declares (checked by tests/test_abi.py)
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
-           "kpd_plan_timing", "kpd_plan_timing_query", "kpd_plan_set_detector", "kpd_bench_conv16",
+           "kpd_plan_timing", "kpd_plan_timing_stage", "kpd_plan_timing_query", "kpd_plan_set_detector",
+           "kpd_bench_conv16",
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
@@ -66,6 +67,7 @@ def load() -> ctypes.CDLL:
     lib.kpd_debug_copy.argtypes = [c_void_p, c_char_p, c_void_p, ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t), c_void_p]
     lib.kpd_plan_timing.argtypes = [c_void_p, c_int]
+    lib.kpd_plan_timing_stage.argtypes = [c_void_p, c_char_p]
     lib.kpd_plan_timing_query.argtypes = [c_void_p, c_char_p, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(c_int)]
     lib.kpd_target_heatmaps.argtypes = [c_void_p, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]
@@ -145,7 +147,9 @@ class Plan:
                                        _ptr(vis), _ptr(heat), _ptr(kh_kpts), _ptr(kh_vis), _ptr(box_scores),
                                        _ptr(topk), _stream(self.device)), "kpd_forward")
 
-    def timing(self, enable: bool) -> None:
+    def timing(self, enable: bool, stage: Optional[str] = None) -> None:
+        """Record per-stage HIP events on the launch streams (only ``stage`` if given)."""
+        check(self.lib.kpd_plan_timing_stage(self.h, stage.encode() if stage else None), "kpd_plan_timing_stage")
         check(self.lib.kpd_plan_timing(self.h, 1 if enable else 0), "kpd_plan_timing")
 
     def timing_query(self, stage: str):

@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""Per-GPU throughput of the other BASELINE.json configs (bench.py times C2,
-the metric's config).  One JSON line per config:
+"""Per-GPU throughput / latency of the other BASELINE.json configs (bench.py
+times C2, the metric's config).  One JSON line per config:
+
+  C1  one 256x192 image with one box, as scripts/predict.py runs the forward:
+      synchronous GPU latency (median of 50 after 10 warm-ups) beside the CPU
+      reference path (the golden-pinned oracle, median of 5) on the host's
+      CPU share
 
   C3  B=256, 256x192, no boxes: person-detector glue (max 5 kept) + heatmap
       head + KEYPOINT_HEAD per ROI
@@ -29,6 +34,7 @@ from dll.models import MultiPersonKeypointModel  # noqa: E402
 from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict  # noqa: E402
 
 CONFIGS = {
+    "C1": dict(B=1, H=256, W=192, P=1, desc="1 image 256x192, 1 box (scripts/predict.py forward), latency"),
     "C3": dict(B=256, H=256, W=192, P=None, desc="B=256 256x192, person-detector glue (max 5) + heatmap head + "
                                                  "KEYPOINT_HEAD"),
     "C5": dict(B=256, H=384, W=288, P=5, desc="per-GPU share of B=2048/8, 384x288, 5 boxes/img, heatmap head + "
@@ -36,22 +42,60 @@ CONFIGS = {
 }
 
 
+def c1_latency(m, c, precision):
+    import bench
+    from oracle import kpd_oracle as O
+    dev = torch.device("cuda", 0)
+    img = synthetic_images(1, 3, c["H"], c["W"], seed=7)
+    box = synthetic_boxes(1, 1, seed=8)
+    batch = {"image": img.to(dev), "bboxes": box.to(dev)}
+    ts = []
+    with torch.no_grad():
+        for i in range(60):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = m(batch)
+            torch.cuda.synchronize()
+            if i >= 10:
+                ts.append(time.perf_counter() - t0)
+    ts.sort()
+    ci = bench.host_cpu_info()
+    torch.set_num_threads(ci["threads"])
+    sd = {k: v.cpu() for k, v in m.state_dict().items()}
+    ref = O.forward(sd, {"image": img, "bboxes": box})
+    cs = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        O.forward(sd, {"image": img, "bboxes": box})
+        cs.append(time.perf_counter() - t0)
+    cs.sort()
+    return {"config": "C1", "workload": c["desc"], "precision": precision,
+            "gpu_latency_ms": round(ts[len(ts) // 2] * 1e3, 3), "gpu_latency_p90_ms": round(ts[int(len(ts) * .9)] * 1e3, 3),
+            "cpu_reference_latency_ms": round(cs[2] * 1e3, 2), "cpu_threads": ci["threads"], "cpu_model": ci["model"],
+            "max_abs_dkpt_vs_cpu": float((out["keypoints"].cpu() - ref["keypoints"]).abs().max())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--precision", default="mixed", choices=["fp32", "mixed"])
+    ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"])
     ap.add_argument("--streams", type=int, default=2)
-    ap.add_argument("--configs", default="C3,C5")
+    ap.add_argument("--configs", default="C1,C3,C5")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     for name in a.configs.split(","):
         c = CONFIGS[name]
         m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
-                                     TrainingConfig(), precision=a.precision, dual_head=True, streams=a.streams)
+                                     TrainingConfig(), precision=a.precision, dual_head=name != "C1",
+                                     streams=a.streams)
         m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
         m = m.to(dev).eval()
+        if name == "C1":
+            print(json.dumps(c1_latency(m, c, a.precision)), flush=True)
+            del m
+            continue
         img = synthetic_images(c["B"], 3, c["H"], c["W"], seed=1234).to(dev)
         batch = {"image": img}
         if c["P"]:

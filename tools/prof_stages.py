@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Steady-state per-stage summaries of rocprofv3 runs of bench.py.
+
+    prof_stages.py <rocprof_outdir> --precision split [--skip 2] [--out profiles/r02/x.json]
+
+Dispatches are ordered (Dispatch_Id, else start time) and cut into forwards at
+each stem_kernel launch (the first kernel of every forward); the first --skip
+forwards (plan setup, warm-up) and everything before the first forward
+(weight upload copies, workspace fills) are dropped, so the numbers describe
+the steady state only.  Kernels are labelled with the plan's stage names:
+fpn0x_kernel -> fpn0; hmconv_kernel<64,...> -> hm_conv3; the first / second
+hmconv_kernel<256|128,...> of a forward -> hm_conv1 / hm_conv2.
+
+kernel_trace.csv -> mean / min / max duration per stage and per kernel.
+counter_collection.csv (--pmc passes) -> counters averaged per stage; HBM
+bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950: FETCH_SIZE
+reports half the bytes of 16-byte-per-lane streaming reads, MI355X_MICROARCH.md
+§HBM); MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
+GRBM_GUI_ACTIVE / 8 XCDs).  Writes JSON keyed "<stage>:<precision>" (the key
+bench.py --pmc-json reads) plus per-kernel entries.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0] if "(" in n else n
+
+
+def label(forward):
+    """Stage label per dispatch of one forward (list of kernel names)."""
+    out, hm = [], 0
+    for k in forward:
+        if k.startswith("fpn0x_kernel"):
+            out.append("fpn0")
+        elif k.startswith("hmconv_kernel<64"):
+            out.append("hm_conv3")
+        elif k.startswith("hmconv_kernel<"):
+            hm += 1
+            out.append("hm_conv1" if hm == 1 else "hm_conv2")
+        else:
+            out.append(None)
+    return out
+
+
+def forwards(rows, key):
+    """rows: list of (order, name, payload) -> list of forwards [(name, payload), ...]."""
+    rows.sort(key=key)
+    fw, cur = [], None
+    for r in rows:
+        if r[1].startswith("stem_kernel"):
+            cur = []
+            fw.append(cur)
+        if cur is not None:
+            cur.append((r[1], r[2]))
+    return fw
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("outdir")
+    ap.add_argument("--precision", default="split")
+    ap.add_argument("--skip", type=int, default=2)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = {"_meta": {"source": a.outdir, "precision": a.precision, "skip_forwards": a.skip}}
+    # ---- kernel trace
+    kt = []
+    tdir = os.path.join(a.outdir, "trace") if os.path.isdir(os.path.join(a.outdir, "trace")) else a.outdir
+    for f in glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                kt.append((t0, short(r["Kernel_Name"]), (t1 - t0) * 1e-3))
+    if kt:
+        fw = forwards(kt, key=lambda r: r[0])[a.skip:]
+        st, kn = defaultdict(list), defaultdict(list)
+        for f in fw:
+            for (name, us), lab in zip(f, label([n for n, _ in f])):
+                kn[name].append(us)
+                if lab:
+                    st[lab].append(us)
+        res["_meta"]["forwards_traced"] = len(fw)
+        res["_meta"]["forward_kernel_us"] = round(sum(sum(v) for v in kn.values()) / max(len(fw), 1), 2)
+        for lab, v in st.items():
+            res[f"{lab}:{a.precision}"] = {"avg_us": round(sum(v) / len(v), 3), "min_us": round(min(v), 3),
+                                           "max_us": round(max(v), 3), "launches": len(v)}
+        res["kernels_us"] = {k: {"avg_us": round(sum(v) / len(v), 3), "calls": len(v),
+                                 "per_forward_us": round(sum(v) / max(len(fw), 1), 3)}
+                             for k, v in sorted(kn.items(), key=lambda kv: -sum(kv[1]))}
+    # ---- counters
+    disp = defaultdict(dict)
+    names = {}
+    for f in glob.glob(os.path.join(a.outdir, "**", "*counter_collection.csv"), recursive=True):
+        tag = os.path.relpath(f, a.outdir).split(os.sep)[0]
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("Counter_Value") in (None, ""):
+                    continue
+                did = (tag, int(r.get("Dispatch_Id") or r.get("Correlation_Id")))
+                disp[did][r["Counter_Name"]] = disp[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                names[did] = short(r["Kernel_Name"])
+    if disp:
+        per_tag = defaultdict(list)
+        for (tag, did), cs in disp.items():
+            per_tag[tag].append((did, names[(tag, did)], cs))
+        agg = defaultdict(lambda: defaultdict(list))
+        for tag, rows in per_tag.items():
+            for f in forwards(rows, key=lambda r: r[0])[a.skip:]:
+                for (name, cs), lab in zip(f, label([n for n, _ in f])):
+                    for c, v in cs.items():
+                        if lab:
+                            agg[f"{lab}:{a.precision}"][c].append(v)
+                        agg[name][c].append(v)
+        for k, cs in agg.items():
+            e = res.setdefault(k, {}) if ":" in k else res.setdefault("counters", {}).setdefault(k, {})
+            for c, v in cs.items():
+                e[c] = sum(v) / len(v)
+            if "FETCH_SIZE" in e or "WRITE_SIZE" in e:
+                e["hbm_bytes_per_launch"] = 2 * e.get("FETCH_SIZE", 0.0) * 1024 + e.get("WRITE_SIZE", 0.0) * 1024
+            if e.get("SQ_VALU_MFMA_BUSY_CYCLES") and e.get("GRBM_GUI_ACTIVE"):
+                e["mfma_busy_frac"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"])
+            if ":" in k:
+                e["source"] = a.outdir
+    txt = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(txt)
+    for k, e in res.items():
+        if ":" in k:
+            print(k, {c: (round(v, 4) if isinstance(v, float) else v) for c, v in e.items()
+                      if c in ("avg_us", "min_us", "launches", "hbm_bytes_per_launch", "mfma_busy_frac",
+                               "FETCH_SIZE", "WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE")})
+
+
+if __name__ == "__main__":
+    main()
