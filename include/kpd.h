@@ -64,6 +64,12 @@ int kpd_plan_finalize(kpd_plan* plan, int precision);
 
 void kpd_plan_destroy(kpd_plan* plan);
 
+/* HeatmapHead stages (kpd_heatmap_head) */
+#define KPD_HEAD_CHANNEL_ATT 1
+#define KPD_HEAD_SPATIAL_ATT 2
+#define KPD_HEAD_CONVS 4
+#define KPD_HEAD_ALL 7
+
 #define KPD_FLAG_DETECT 1     /* no caller boxes: person detector + NMS WRITE boxes [B][P][4] */
 #define KPD_FLAG_DUAL_HEAD 2  /* also run KEYPOINT_HEAD on 128-ch ROI features */
 
@@ -170,6 +176,66 @@ int kpd_plan_set_streams(kpd_plan* plan, int n);
  * dbg: 0 full kernel, 1 without the K-loop loads, 2 without the MFMAs,
  * 4 with an L2-resident A working set.  *ms = mean time per launch. */
 int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cout, int dbg, int iters, float* ms);
+
+/* ---- Stand-alone operators: the reference's submodule forwards and helper
+ * functions, for callers that use them outside MultiPersonKeypointModel.forward.
+ * Tensors are NCHW fp32 device memory, exactly as the reference modules take
+ * and return them.  Plan-based entries need a plan holding that submodule's
+ * weights under the model's state-dict names (a partial plan is fine: a
+ * finalize packs the components it finds -- backbone.body, backbone.fpn,
+ * channel_attention, heatmap_head, person_detector, keypoint_head). */
+
+/* HeatmapHead.forward (heatmap_head.py:81-113): x [R][64][56][56] ->
+ * heat [R][17][56][56] (sigmoid maps); attention weights ch_w [R][64] and
+ * sp_w [R][56][56] (nullable).  parts = KPD_HEAD_* selects the stages: a
+ * disabled attention uses weights 1 (use_attention=False), parts without
+ * KPD_HEAD_CONVS computes only the attention weights (the attention modules'
+ * own forwards, :129-151). */
+int kpd_heatmap_head(kpd_plan* plan, const float* x, int R, int H, int W, int parts, float* heat, float* ch_w,
+                     float* sp_w, void* stream);
+
+/* KEYPOINT_HEAD.forward (keypoint_head.py:50-62): x [R][128][56][56] ->
+ * keypoints [R][17][2], visibility [R][17][3] (sigmoid outputs). */
+int kpd_keypoint_head(kpd_plan* plan, const float* x, int R, int H, int W, float* keypoints, float* visibility,
+                      void* stream);
+
+/* MobileNetV3Wrapper.forward (backbone.py:258-264 + LightweightFPN :29-39):
+ * image [B][C][H][W] -> the four FPN levels out_i [B][128][h_i][w_i] at the
+ * strides of features.0 / .3 / .8 / .12 (2, 8, 16, 32). */
+int kpd_backbone(kpd_plan* plan, const float* image, int B, int C, int H, int W, float* out0, float* out1,
+                 float* out2, float* out3, void* stream);
+
+/* ChannelAttention.forward (keypoint_model.py:33-44) on x [B][128][H][W] ->
+ * scores [B][128] (sigmoid); select_top_k_channels (:653-661): topk [B][k]
+ * int32 (descending score, ties to the lower index) and selected
+ * [B][k][H][W] = x[b, topk[b]] (both nullable).  k = 64. */
+int kpd_channel_attention(kpd_plan* plan, const float* x, int B, int C, int H, int W, float* scores, int32_t* topk,
+                          int k, float* selected, void* stream);
+
+/* Heatmap decoders over `planes` maps of H x W (device):
+ *   KPD_DECODE_ARGMAX     decode_heatmaps (heatmap_head.py:265-296)
+ *   KPD_DECODE_SUBPIXEL   decode_heatmaps_subpixel (:298-370), param = window size
+ *   KPD_DECODE_SOFTARGMAX decode_heatmaps_soft_argmax (:372-413), param = temperature
+ *   KPD_DECODE_MODEL      MultiPersonKeypointModel.decode_heatmap (keypoint_model.py:250-313):
+ *                         soft-argmax + 3-class visibility vis [planes][3]
+ * keypoints [planes][2] normalised, scores [planes] (the maximum; nullable). */
+#define KPD_DECODE_ARGMAX 0
+#define KPD_DECODE_SUBPIXEL 1
+#define KPD_DECODE_SOFTARGMAX 2
+#define KPD_DECODE_MODEL 3
+int kpd_decode_heatmaps(const float* heat, int planes, int H, int W, int mode, float param, float* keypoints,
+                        float* scores, float* vis, void* stream);
+
+/* torchvision.ops.roi_align as extract_roi_features calls it
+ * (keypoint_model.py:212-228): features [B][C][H][W], rois [R][5] =
+ * (batch index, x1, y1, x2, y2) -> out [R][C][out_h][out_w]. */
+int kpd_roi_align(const float* features, int B, int C, int H, int W, const float* rois, int R, int out_h, int out_w,
+                  float spatial_scale, int sampling_ratio, int aligned, float* out, void* stream);
+
+/* 1x1 convolution with bias on NCHW (PERSON_HEAD.forward's box head,
+ * person_head.py:141-166): out [B][Cout][HW] = w [Cout][Cin] . x [B][Cin][HW] + b. */
+int kpd_conv1x1(const float* x, int B, int Cin, int HW, const float* w, const float* b, int Cout, float* out,
+                void* stream);
 
 #ifdef __cplusplus
 }

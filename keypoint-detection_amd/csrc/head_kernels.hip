@@ -337,7 +337,8 @@ __global__ __launch_bounds__(64) void hm_spool_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
                                                        const float* __restrict__ smap, const float* __restrict__ saw,
                                                        const float* __restrict__ sab, void* __restrict__ xs,
-                                                       int out_bf16, const float* __restrict__ hsc) {
+                                                       int out_bf16, const float* __restrict__ hsc, int use_sp,
+                                                       float* __restrict__ sw_out) {
   constexpr int NI = HM / 4;
   __shared__ float w[98];
   __shared__ float2 srow[7][HM + 6];   // the 7 smap rows around y, zero-padded by 3 columns
@@ -382,7 +383,8 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
         a = fmaf(w[49 + ky * 7 + kx], sv2.y, a);
       }
     }
-    ssw[x] = kpd_sigmoid(a + sab[0]);
+    ssw[x] = use_sp ? kpd_sigmoid(a + sab[0]) : 1.f;
+    if (sw_out) sw_out[((size_t)r * HM + y) * HM + x] = ssw[x];
   }
   const float4 cq = reinterpret_cast<const float4*>(cw + (size_t)r * TOPK)[c];
   const float ssc = out_bf16 == 3 ? ldexpf(1.f, split_exp_of(hsc[(size_t)r * 4])) : 1.f;
@@ -558,8 +560,10 @@ hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap
   return hipGetLastError();
 }
 hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
-                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st, const float* hsc) {
-  hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16, hsc);
+                            const float* sab, int R, void* xs, int out_bf16, hipStream_t st, const float* hsc,
+                            int use_sp, float* sw_out) {
+  hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16, hsc,
+                     use_sp, sw_out);
   return hipGetLastError();
 }
 hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot, int P,

@@ -218,9 +218,11 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0,
                             const float* w2, const float* b2, float* cw, float* hsc, hipStream_t st);
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st);
+// use_sp = 0: no spatial attention (weights 1); sw_out != null: the spatial
+// weights [R][56][56] (HeatmapHead.forward's attention_weights[1])
 hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
                             const float* sab, int R, void* xs, int out_bf16, hipStream_t st,
-                            const float* hsc = nullptr);
+                            const float* hsc = nullptr, int use_sp = 1, float* sw_out = nullptr);
 hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot,
                            int P, float* heat_out, hipStream_t st);
 hipError_t launch_decode(const float* heat_out, const float* boxes, const int32_t* slot, int R, int P,
@@ -250,3 +252,19 @@ hipError_t launch_kh_final(const float* lin_r, int r_stride, const float* lin_v,
 // error reporting shared with the C ABI entry points outside kpd_plan.hip
 int kpd_fail_einval(const char* msg);
 int kpd_fail_hip(hipError_t e, const char* where);
+
+// ---- stand-alone operators (ops_kernels.hip) ----
+// mode: KPD_DECODE_* (include/kpd.h)
+hipError_t launch_decode_planes(const float* heat, int planes, int H, int W, int mode, float param, float* kpts,
+                                float* scores, float* vis, hipStream_t st);
+hipError_t launch_roi_align_nchw(const float* feat, int C, int H, int W, const float* rois, int R, int oh, int ow,
+                                 float scale, int sr, int aligned, float* out, hipStream_t st);
+hipError_t launch_nchw_rows_to_nhwc(const float* in, int N, int C, int H, int W, float* out, float* stats,
+                                    hipStream_t st);
+hipError_t launch_nhwc_to_nchw(const float* in, int N, int HW, int C, float* out, hipStream_t st);
+hipError_t launch_nchw_channel_stats(const float* x, int N, int C, int HW, float* stats, hipStream_t st);
+hipError_t launch_gather_planes(const float* x, int N, int C, int HW, const int32_t* idx, int K, float* out,
+                                hipStream_t st);
+hipError_t launch_conv1x1_nchw(const float* x, int N, int Cin, int HW, const float* w, const float* b, int Cout,
+                               float* out, hipStream_t st);
+hipError_t launch_fill(float* p, long n, float v, hipStream_t st);

@@ -169,6 +169,8 @@ struct kpd_plan {
   DevConv last;
   DevConv lat[4];
   DevConv fpn0;
+  DevConv fpn_lv[3];   // fpn_convs.1-3 (MobileNetV3Wrapper.forward only; the model's forward skips them)
+  bool has_body = false, has_fpn = false, has_ca = false, has_hm = false;   // components registered
   float *ca_w0 = nullptr, *ca_b0 = nullptr, *ca_w2 = nullptr, *ca_b2 = nullptr;
   float *hca_w0 = nullptr, *hca_b0 = nullptr, *hca_w2 = nullptr, *hca_b2 = nullptr;
   float *sa_w = nullptr, *sa_b = nullptr;
@@ -195,11 +197,12 @@ struct kpd_plan {
   float *kh_lnv_g = nullptr, *kh_lnv_b = nullptr, *kh_fv_w = nullptr, *kh_fv_b = nullptr;
   // workspace, one per concurrent sub-batch (kpd_plan_set_streams)
   static constexpr int kMaxSub = 4;
-  void* ws[kMaxSub] = {};
-  size_t ws_bytes[kMaxSub] = {};
-  Dims dims[kMaxSub];
-  Work work[kMaxSub];
-  bool have_work[kMaxSub] = {};
+  static constexpr int kOpWs = kMaxSub;   // workspace of the stand-alone operator entry points
+  void* ws[kMaxSub + 1] = {};
+  size_t ws_bytes[kMaxSub + 1] = {};
+  Dims dims[kMaxSub + 1];
+  Work work[kMaxSub + 1];
+  bool have_work[kMaxSub + 1] = {};
   int streams = 1;                        // requested sub-batch streams (kpd_plan_set_streams)
   hipStream_t sub_st[kMaxSub] = {};       // [0] unused: sub-batch 0 runs on the caller's stream
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
@@ -738,8 +741,9 @@ void kpd_plan_destroy(kpd_plan* p) {
   int cur = 0;
   if (hipGetDevice(&cur) == hipSuccess) (void)hipSetDevice(p->device);
   for (void* a : p->allocs) (void)hipFree(a);
-  for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
+  for (int k = 0; k <= kpd_plan::kMaxSub; ++k)
     if (p->ws[k]) (void)hipFree(p->ws[k]);
+  for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
     if (p->sub_st[k]) (void)hipStreamDestroy(p->sub_st[k]);
     if (p->join_ev[k]) (void)hipEventDestroy(p->join_ev[k]);
   }
@@ -764,10 +768,11 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   p->hm1 = DevConv();
   p->hm2 = DevConv();
   p->hm3 = DevConv();
+  for (auto& c : p->fpn_lv) c = DevConv();
   p->kh_ds1 = DevConv();
   p->kh_ds2 = DevConv();
   p->has_kh = false;
-  for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
+  for (int k = 0; k <= kpd_plan::kMaxSub; ++k) {
     if (p->ws[k]) { (void)hipFree(p->ws[k]); p->ws[k] = nullptr; p->ws_bytes[k] = 0; }
     p->have_work[k] = false;
   }
@@ -775,9 +780,21 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   std::string missing;
   int rc = KPD_OK;
   auto chk = [&](int r) { if (r != KPD_OK && rc == KPD_OK) rc = r; };
+  // Components present in the registered state dict (a submodule's own plan
+  // -- HeatmapHead, KEYPOINT_HEAD, the backbone -- registers only its part);
+  // a present component must be complete.
+  auto has = [&](const char* prefix) {
+    auto it = p->t.lower_bound(prefix);
+    return it != p->t.end() && it->first.compare(0, strlen(prefix), prefix) == 0;
+  };
+  p->has_body = has("backbone.body.");
+  p->has_fpn = has("backbone.fpn.");
+  p->has_ca = has("channel_attention.");
+  p->has_hm = has("heatmap_head.");
+  const bool has_pd = has("person_detector.");
   const std::string F = "backbone.body.features.";
   // stem: [16][Cin][3][3] + BN, packed [16][Cin*9]
-  {
+  if (p->has_body) {
     const HostT* w = get(p, F + "0.0.weight", missing);
     const HostT *g = get(p, F + "0.1.weight", missing), *b = get(p, F + "0.1.bias", missing);
     const HostT *m = get(p, F + "0.1.running_mean", missing), *v = get(p, F + "0.1.running_var", missing);
@@ -797,7 +814,6 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     } else {
       chk(KPD_ESTATE);
     }
-  }
   for (int i = 0; i < 11; ++i) {
     DevBneck& bn = p->bn[i];
     bn.cfg = kBneck[i];
@@ -823,17 +839,29 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     chk(pack_conv(p, pj + ".0.weight", "", pj + ".1", 1e-3, 1, false, bn.project, missing));
   }
   chk(pack_conv(p, F + "12.0.weight", "", F + "12.1", 1e-3, 1, false, p->last, missing));
+  }
+  if (p->has_fpn) {
   for (int i = 0; i < 4; ++i)
     chk(pack_conv(p, "backbone.fpn.lateral_convs." + std::to_string(i) + ".weight", "", "", 0, 1, false,
                   p->lat[i], missing));
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
   if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty()) chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
+  // levels 1-3 (dead in the model's forward; MobileNetV3Wrapper.forward returns them)
+  for (int i = 1; i < 4; ++i) {
+    const std::string c = "backbone.fpn.fpn_convs." + std::to_string(i);
+    if (p->t.count(c + ".0.weight"))
+      chk(pack_conv(p, c + ".0.weight", "", c + ".1", 1e-5, 3, false, p->fpn_lv[i - 1], missing));
+  }
+  }
+  if (p->has_ca) {
   chk(pack_plain(p, "channel_attention.fc.0.weight", &p->ca_w0, missing, 8 * 128));
   chk(pack_plain(p, "channel_attention.fc.0.bias", &p->ca_b0, missing, 8));
   chk(pack_plain(p, "channel_attention.fc.2.weight", &p->ca_w2, missing, 128 * 8));
   chk(pack_plain(p, "channel_attention.fc.2.bias", &p->ca_b2, missing, 128));
+  }
   const std::string Hh = "heatmap_head.";
+  if (p->has_hm) {
   chk(pack_plain(p, Hh + "channel_attention.fc.0.weight", &p->hca_w0, missing, 4 * 64));
   chk(pack_plain(p, Hh + "channel_attention.fc.0.bias", &p->hca_b0, missing, 4));
   chk(pack_plain(p, Hh + "channel_attention.fc.2.weight", &p->hca_w2, missing, 64 * 4));
@@ -854,12 +882,13 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   }
   chk(pack_plain(p, Hh + "final_layer.3.weight", &p->fin_w, missing, 17 * 64));
   chk(pack_plain(p, Hh + "final_layer.3.bias", &p->fin_b, missing, 17));
+  }
   {
     std::vector<float> z(128, 0.f);
     chk(upload(p, z, &p->zero_bias));
   }
   // person-detector glue: box_heads[0] ++ cls_heads[0] -> one 1x1 conv (45 outputs)
-  {
+  if (has_pd) {
     const HostT* bw = get(p, "person_detector.box_heads.0.weight", missing);
     const HostT* bb = get(p, "person_detector.box_heads.0.bias", missing);
     const HostT* cw = get(p, "person_detector.cls_heads.0.weight", missing);
@@ -926,10 +955,10 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   if (!missing.empty()) return fail(KPD_ESTATE, "missing tensors: " + missing);
   if (rc != KPD_OK) return rc;
   // shape checks the kernels rely on
-  if (p->fpn0.cin != 128 || p->fpn0.cout != 128) return fail(KPD_EINVAL, "fpn_convs.0 must be 128->128");
-  if (p->hm1.cin != 64 || p->hm3.cout != 64 || p->hm1.cout != p->hm2.cin || p->hm2.cout != p->hm3.cin)
+  if (p->has_fpn && (p->fpn0.cin != 128 || p->fpn0.cout != 128)) return fail(KPD_EINVAL, "fpn_convs.0 must be 128->128");
+  if (p->has_hm && (p->hm1.cin != 64 || p->hm3.cout != 64 || p->hm1.cout != p->hm2.cin || p->hm2.cout != p->hm3.cin))
     return fail(KPD_EINVAL, "heatmap head channel chain mismatch");
-  if (p->bn[0].cfg.cin != 16) return fail(KPD_EINVAL, "bad body");
+  if (p->has_body && p->bn[0].cfg.cin != 16) return fail(KPD_EINVAL, "bad body");
   p->finalized = true;
   return KPD_OK;
 }
@@ -968,6 +997,98 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   if (hm_padded(p)) HIP_TRY(hipMemsetAsync(p->ws[k], 0, need, st));
   p->dims[k] = d;
   p->have_work[k] = true;
+  return KPD_OK;
+}
+
+// HeatmapHead (heatmap_head.py:81-151) on the [R][56][56][64] NHWC ROI
+// features in w.roi with their per-row statistics in w.roi_stats: channel
+// attention, spatial attention, the three 3x3 convs and the final 1x1 +
+// sigmoid, heatmaps written at the ROIs' slots (w.slot, P).  parts selects
+// the stages (KPD_HEAD_*; a disabled attention uses weights 1); sw_out
+// (nullable) receives the spatial weights [R][56][56].
+static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out, hipStream_t st, int parts,
+                            float* sw_out, unsigned long long* stamps2, unsigned long long* stamps3) {
+  std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
+  // split: per-ROI operand bounds, hsc[r] = {max|xs| (written here), max|h1| (conv 1)}
+  const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
+  HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw,
+                           hsplit ? w.hsc : nullptr, st));
+  if (!(parts & KPD_HEAD_CHANNEL_ATT)) HIP_TRY(launch_fill(w.cw, (long)R * 64, 1.f, st));
+  HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
+  const bool bf = p->precision == KPD_PRECISION_MIXED;
+  const int xs_mode = hsplit ? 3 : bf ? (hm_padded(p) ? 2 : 1) : 0;
+  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc,
+                           (parts & KPD_HEAD_SPATIAL_ATT) != 0, sw_out));
+  att_stage.reset();
+  if (!(parts & KPD_HEAD_CONVS)) return KPD_OK;
+  // bounds: |xs| <= U0; |h1| <= bc1 + bs1 U0; |h2| <= bc2 + bs2 max|h1| (the
+  // exponent each producer scales by and its consumer unscales by)
+  const HmSplit sp1{w.hsc, 0.f, 1.f, 0, p->hm1.bc, p->hm1.bs, 0, 1};
+  const HmSplit sp2{w.hsc, p->hm1.bc, p->hm1.bs, 0, p->hm2.bc, p->hm2.bs, 1, -1};
+  const HmSplit sp3{w.hsc, p->hm2.bc, p->hm2.bs, 1, 0.f, 0.f, -1, -1};
+  std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
+  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st, nullptr, nullptr, &sp1)) return rc;
+  c1.reset();
+  std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
+  if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st, nullptr, stamps2, &sp2))
+    return rc;
+  c2.reset();
+  std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
+  // mixed / split: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
+  static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
+  const bool fin_fused = (p->hm3.bf16 || p->hm3.ws) && p->hm3.cout_p == 64 && (!no_fin_fuse || p->hm3.ws);
+  const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
+  if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr, stamps3, &sp3))
+    return rc;
+  c3.reset();
+  if (!fin_fused) HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
+  return KPD_OK;
+}
+
+// KEYPOINT_HEAD (keypoint_head.py:50-62, ResidualBlock :64-90) on the
+// [R][56][56][128] NHWC ROI features in w.kx; outputs at the ROIs' slots.
+static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st) {
+  const size_t px = (size_t)R * 3136;
+  if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+    return rc;
+  HIP_TRY(launch_kh_att(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, px, st));
+  // ResidualBlock(128 -> 64): relu6(relu6(bn1(relu6(conv_bn(x)))) + downsample(x))
+  const float* id1 = w.kx;
+  if (p->kh_ds1.w) {
+    if (int rc = conv(p->kh_ds1, w.kx, R, 56, 56, 128, w.kds1, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    id1 = w.kds1;
+  }
+  if (int rc = conv_post(p->kh_rb1, w.kx, R, 56, 56, 128, w.krb1, ACT_RELU6, p->kh_bn1a_s, p->kh_bn1a_t,
+                         ACT_RELU6, id1, ACT_RELU6, st))
+    return rc;
+  const float* id2 = w.krb1;
+  if (p->kh_ds2.w) {
+    if (int rc = conv(p->kh_ds2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.kds2, ACT_NONE, nullptr, 0, 0, nullptr,
+                      nullptr, 0, 0, st))
+      return rc;
+    id2 = w.kds2;
+  }
+  if (int rc = conv_post(p->kh_rb2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.krb2, ACT_RELU6, p->kh_bn1b_s,
+                         p->kh_bn1b_t, ACT_RELU6, id2, ACT_RELU6, st))
+    return rc;
+  if (int rc = conv(p->kh_c3, w.krb2, R, 56, 56, p->kh_rb2.cout_p, w.kr3, ACT_RELU6, nullptr, 0, 0, nullptr,
+                    nullptr, 0, 0, st))
+    return rc;
+  if (int rc = conv(p->kh_v1, w.kx, R, 56, 56, 128, w.kv1, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+    return rc;
+  const int o = p->kh_o, kr = pad16(16 * o * o);
+  if (kr != 16 * o * o) HIP_TRY(hipMemsetAsync(w.kpr, 0, sizeof(float) * R * kr, st));
+  HIP_TRY(launch_kh_pool(w.kr3, R, 16, o, w.kpr, kr, st));
+  HIP_TRY(launch_kh_pool(w.kv1, R, 32, 4, w.kpv, 512, st));
+  // the two Linear layers as 1x1 MFMA GEMMs over all ROIs (M = R)
+  if (int rc = conv(p->kh_lr, w.kpr, R, 1, 1, kr, w.klr, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+    return rc;
+  if (int rc = conv(p->kh_lv, w.kpv, R, 1, 1, 512, w.klv, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+    return rc;
+  HIP_TRY(launch_kh_final(w.klr, p->kh_lr.cout_p, w.klv, p->kh_lv.cout_p, p->kh_lnr_g, p->kh_lnr_b, p->kh_fr_w,
+                          p->kh_fr_b, p->kh_lnv_g, p->kh_lnv_b, p->kh_fv_w, p->kh_fv_b, w.slot, R, P, kh_kpts,
+                          kh_vis, st));
   return KPD_OK;
 }
 
@@ -1202,6 +1323,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   }
   fpn_stage.reset();
   std::unique_ptr<Stage> topk_stage(new Stage(p, "topk", st));
+  if (!p->has_ca) return KPD_OK;   // backbone-only plan (kpd_backbone)
   if (!d.fused_stats) HIP_TRY(launch_channel_stats(w.feat, B, HWf, 128, d.tiles, w.stats, st));
   // given boxes for every image: the slot map rides along with the top-k launch
   const bool slot_in_topk = !detect && NB == B && NB * P > 0 && boxes != nullptr;
@@ -1243,88 +1365,19 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
   }
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
-  std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
-  // split: per-ROI operand bounds, hsc[r] = {max|xs| (written here), max|h1| (conv 1)}
-  const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
-  HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw,
-                           hsplit ? w.hsc : nullptr, st));
-  HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
-  const bool bf = p->precision == KPD_PRECISION_MIXED;
-  const int xs_mode = hsplit ? 3 : bf ? (hm_padded(p) ? 2 : 1) : 0;
-  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc));
-  att_stage.reset();
-  // bounds: |xs| <= U0; |h1| <= bc1 + bs1 U0; |h2| <= bc2 + bs2 max|h1| (the
-  // exponent each producer scales by and its consumer unscales by)
-  const HmSplit sp1{w.hsc, 0.f, 1.f, 0, p->hm1.bc, p->hm1.bs, 0, 1};
-  const HmSplit sp2{w.hsc, p->hm1.bc, p->hm1.bs, 0, p->hm2.bc, p->hm2.bs, 1, -1};
-  const HmSplit sp3{w.hsc, p->hm2.bc, p->hm2.bs, 1, 0.f, 0.f, -1, -1};
-  std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
-  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st, nullptr, nullptr, &sp1)) return rc;
-  c1.reset();
-  std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
-  if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st, nullptr,
-                       take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2), &sp2))
+  if (int rc = run_heatmap_head(p, w, R, P, heat_out, st, KPD_HEAD_ALL, nullptr,
+                                 take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
+                                 take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
     return rc;
-  c2.reset();
-  std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
-  // mixed / split: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
-  static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
-  const bool fin_fused = (p->hm3.bf16 || p->hm3.ws) && p->hm3.cout_p == 64 && (!no_fin_fuse || p->hm3.ws);
-  const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
-  if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr,
-                       take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2), &sp3))
-    return rc;
-  c3.reset();
   {
     Stage sg(p, "hm_final_decode", st);
-    if (!fin_fused) HIP_TRY(launch_hm_final(w.h3, R, p->fin_w, p->fin_b, w.slot, P, heat_out, st));
     HIP_TRY(launch_decode(heat_out, boxes, w.slot, R, P, kpts, vis, st));
   }
   if (dual) {
     // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
     Stage sg(p, "keypoint_head", st);
-    const size_t px = (size_t)R * 3136;
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
-    if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-      return rc;
-    HIP_TRY(launch_kh_att(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, px, st));
-    // ResidualBlock(128 -> 64): relu6(relu6(bn1(relu6(conv_bn(x)))) + downsample(x))
-    const float* id1 = w.kx;
-    if (p->kh_ds1.w) {
-      if (int rc = conv(p->kh_ds1, w.kx, R, 56, 56, 128, w.kds1, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-        return rc;
-      id1 = w.kds1;
-    }
-    if (int rc = conv_post(p->kh_rb1, w.kx, R, 56, 56, 128, w.krb1, ACT_RELU6, p->kh_bn1a_s, p->kh_bn1a_t,
-                           ACT_RELU6, id1, ACT_RELU6, st))
-      return rc;
-    const float* id2 = w.krb1;
-    if (p->kh_ds2.w) {
-      if (int rc = conv(p->kh_ds2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.kds2, ACT_NONE, nullptr, 0, 0, nullptr,
-                        nullptr, 0, 0, st))
-        return rc;
-      id2 = w.kds2;
-    }
-    if (int rc = conv_post(p->kh_rb2, w.krb1, R, 56, 56, p->kh_rb1.cout_p, w.krb2, ACT_RELU6, p->kh_bn1b_s,
-                           p->kh_bn1b_t, ACT_RELU6, id2, ACT_RELU6, st))
-      return rc;
-    if (int rc = conv(p->kh_c3, w.krb2, R, 56, 56, p->kh_rb2.cout_p, w.kr3, ACT_RELU6, nullptr, 0, 0, nullptr,
-                      nullptr, 0, 0, st))
-      return rc;
-    if (int rc = conv(p->kh_v1, w.kx, R, 56, 56, 128, w.kv1, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-      return rc;
-    const int o = p->kh_o, kr = pad16(16 * o * o);
-    if (kr != 16 * o * o) HIP_TRY(hipMemsetAsync(w.kpr, 0, sizeof(float) * R * kr, st));
-    HIP_TRY(launch_kh_pool(w.kr3, R, 16, o, w.kpr, kr, st));
-    HIP_TRY(launch_kh_pool(w.kv1, R, 32, 4, w.kpv, 512, st));
-    // the two Linear layers as 1x1 MFMA GEMMs over all ROIs (M = R)
-    if (int rc = conv(p->kh_lr, w.kpr, R, 1, 1, kr, w.klr, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-      return rc;
-    if (int rc = conv(p->kh_lv, w.kpv, R, 1, 1, 512, w.klv, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-      return rc;
-    HIP_TRY(launch_kh_final(w.klr, p->kh_lr.cout_p, w.klv, p->kh_lv.cout_p, p->kh_lnr_g, p->kh_lnr_b, p->kh_fr_w,
-                            p->kh_fr_b, p->kh_lnv_g, p->kh_lnv_b, p->kh_fv_w, p->kh_fv_b, w.slot, R, P, kh_kpts,
-                            kh_vis, st));
+    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st)) return rc;
   }
   return KPD_OK;
 }
@@ -1334,6 +1387,8 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
                 int32_t* topk_out, void* stream) {
   if (!p) return fail(KPD_EINVAL, "null plan");
   if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_body || !p->has_fpn || !p->has_ca || !p->has_hm)
+    return fail(KPD_ESTATE, "plan lacks backbone / fpn / channel_attention / heatmap_head weights");
   if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
   if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
   if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD)) return fail(KPD_EINVAL, "unknown flags");
@@ -1452,6 +1507,145 @@ int kpd_debug_copy(kpd_plan* p, const char* name, void* dst, size_t bytes, size_
   if (bytes < it->second.second) return fail(KPD_EINVAL, "destination too small");
   HIP_TRY(hipMemcpyAsync(dst, it->second.first, it->second.second, hipMemcpyDeviceToDevice,
                          reinterpret_cast<hipStream_t>(stream)));
+  return KPD_OK;
+}
+
+// ---------------------------------------------------------------- stand-alone operators
+// The reference's submodule forwards, called outside the model's forward
+// (each on a plan holding that submodule's weights).
+
+static int op_work(kpd_plan* p, int R, int flags, hipStream_t st, Work** w) {
+  Dims d;
+  d.B = 0; d.NB = R; d.P = 1; d.flags = flags;
+  if (int rc = ensure_work(p, d, kpd_plan::kOpWs, st)) return rc;
+  *w = &p->work[kpd_plan::kOpWs];
+  return KPD_OK;
+}
+
+int kpd_heatmap_head(kpd_plan* p, const float* x, int R, int H, int W, int parts, float* heat, float* ch_w,
+                     float* sp_w, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_hm) return fail(KPD_ESTATE, "plan has no heatmap_head weights");
+  if (R < 0 || H != 56 || W != 56) return fail(KPD_EINVAL, "HeatmapHead input must be [R][64][56][56]");
+  if (parts & ~KPD_HEAD_ALL) return fail(KPD_EINVAL, "unknown HeatmapHead parts");
+  if (R == 0) return KPD_OK;
+  if (!x || ((parts & KPD_HEAD_CONVS) && !heat)) return fail(KPD_EINVAL, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  Work* w = nullptr;
+  if (int rc = op_work(p, R, 0, st, &w)) return rc;
+  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 64, 56, 56, w->roi, w->roi_stats, st));
+  HIP_TRY(hipMemsetAsync(w->slot, 0, sizeof(int32_t) * R, st));   // ROI r -> heat[r] (P = 1)
+  if (int rc = run_heatmap_head(p, *w, R, 1, heat, st, parts, sp_w, nullptr, nullptr)) return rc;
+  if (ch_w) HIP_TRY(hipMemcpyAsync(ch_w, w->cw, sizeof(float) * R * 64, hipMemcpyDeviceToDevice, st));
+  return KPD_OK;
+}
+
+int kpd_keypoint_head(kpd_plan* p, const float* x, int R, int H, int W, float* kpts, float* vis, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_kh) return fail(KPD_ESTATE, "plan has no keypoint_head weights");
+  if (R < 0 || H != 56 || W != 56) return fail(KPD_EINVAL, "KEYPOINT_HEAD input must be [R][128][56][56]");
+  if (R == 0) return KPD_OK;
+  if (!x || !kpts || !vis) return fail(KPD_EINVAL, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  Work* w = nullptr;
+  if (int rc = op_work(p, R, KPD_FLAG_DUAL_HEAD, st, &w)) return rc;
+  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 128, 56, 56, w->kx, nullptr, st));
+  HIP_TRY(hipMemsetAsync(w->slot, 0, sizeof(int32_t) * R, st));
+  return run_keypoint_head(p, *w, R, 1, kpts, vis, st);
+}
+
+int kpd_backbone(kpd_plan* p, const float* image, int B, int C, int H, int W, float* out0, float* out1, float* out2,
+                 float* out3, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_body || !p->has_fpn) return fail(KPD_ESTATE, "plan lacks backbone.body / backbone.fpn weights");
+  for (int i = 0; i < 3; ++i)
+    if (!p->fpn_lv[i].w) return fail(KPD_ESTATE, "plan lacks backbone.fpn.fpn_convs.1-3 weights");
+  if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
+  if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
+  float* outs[4] = {out0, out1, out2, out3};
+  for (float* o : outs)
+    if (!o) return fail(KPD_EINVAL, "null output pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  // level sizes: stem (features.0), features.3, .8, .12 -- as forward_one's Dims
+  int h[12], wd[12];
+  h[0] = (H - 1) / 2 + 1; wd[0] = (W - 1) / 2 + 1;
+  for (int i = 0; i < 11; ++i) {
+    const int k = kBneck[i].k, s = kBneck[i].s, pd = (k - 1) / 2;
+    h[i + 1] = (h[i] + 2 * pd - k) / s + 1;
+    wd[i + 1] = (wd[i] + 2 * pd - k) / s + 1;
+  }
+  const int lh[4] = {h[0], h[3], h[8], h[11]}, lw[4] = {wd[0], wd[3], wd[8], wd[11]};
+  const int cap = max_pass_images(H, W), npass = (B + cap - 1) / cap;
+  for (int q = 0; q < npass; ++q) {
+    const int b0 = (int)((long)B * q / npass), b1 = (int)((long)B * (q + 1) / npass), nb = b1 - b0;
+    if (int rc = forward_one(p, 0, false, image + (size_t)b0 * C * H * W, nb, C, H, W, nullptr, 0, 0, 0, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st))
+      return rc;
+    Work& w = p->work[0];
+    HIP_TRY(launch_nhwc_to_nchw(w.feat, nb, lh[0] * lw[0], 128, outs[0] + (size_t)b0 * 128 * lh[0] * lw[0], st));
+    for (int i = 1; i < 4; ++i) {   // fpn_convs[i] on lateral i (backbone.py:39), into the free level-0 buffer
+      if (int rc = conv(p->fpn_lv[i - 1], w.lat[i], nb, lh[i], lw[i], 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
+                        nullptr, 0, 0, st))
+        return rc;
+      HIP_TRY(launch_nhwc_to_nchw(w.feat, nb, lh[i] * lw[i], 128, outs[i] + (size_t)b0 * 128 * lh[i] * lw[i], st));
+    }
+  }
+  return KPD_OK;
+}
+
+int kpd_channel_attention(kpd_plan* p, const float* x, int B, int C, int H, int W, float* scores, int32_t* topk,
+                          int k, float* selected, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_ca) return fail(KPD_ESTATE, "plan has no channel_attention weights");
+  if (C != 128 || k != 64 || B < 0 || H <= 0 || W <= 0)
+    return fail(KPD_EINVAL, "ChannelAttention path is built for 128 channels and top-64");
+  if (B == 0) return KPD_OK;
+  if (!x) return fail(KPD_EINVAL, "null input");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  char* scratch = nullptr;
+  const size_t sb = (size_t)B * 2 * 128 * 4, tb = (size_t)B * 64 * 4, cb = (size_t)B * 128 * 4;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), sb + tb + cb, st));
+  float* stats = reinterpret_cast<float*>(scratch);
+  int32_t* tk = reinterpret_cast<int32_t*>(scratch + sb);
+  float* sc = reinterpret_cast<float*>(scratch + sb + tb);
+  hipError_t e = launch_nchw_channel_stats(x, B, 128, H * W, stats, st);
+  if (e == hipSuccess)
+    e = launch_topk(stats, B, 1, H * W, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, tk, sc, st, nullptr, 0, nullptr);
+  if (e == hipSuccess && scores) e = hipMemcpyAsync(scores, sc, cb, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && topk) e = hipMemcpyAsync(topk, tk, tb, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && selected) e = launch_gather_planes(x, B, 128, H * W, tk, 64, selected, st);
+  (void)hipFreeAsync(scratch, st);
+  HIP_TRY(e);
+  return KPD_OK;
+}
+
+int kpd_decode_heatmaps(const float* heat, int planes, int H, int W, int mode, float param, float* kpts,
+                        float* scores, float* vis, void* stream) {
+  if (planes < 0 || H < 2 || W < 2 || (planes > 0 && (!heat || !kpts)) || (mode == KPD_DECODE_MODEL && planes > 0 && !vis))
+    return fail(KPD_EINVAL, "bad decode arguments");
+  HIP_TRY(launch_decode_planes(heat, planes, H, W, mode, param, kpts, scores, vis,
+                               reinterpret_cast<hipStream_t>(stream)));
+  return KPD_OK;
+}
+
+int kpd_roi_align(const float* feat, int B, int C, int H, int W, const float* rois, int R, int out_h, int out_w,
+                  float spatial_scale, int sampling_ratio, int aligned, float* out, void* stream) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || R < 0 || out_h <= 0 || out_w <= 0 || (R > 0 && (!feat || !rois || !out)))
+    return fail(KPD_EINVAL, "bad roi_align arguments");
+  HIP_TRY(launch_roi_align_nchw(feat, C, H, W, rois, R, out_h, out_w, spatial_scale, sampling_ratio, aligned, out,
+                                reinterpret_cast<hipStream_t>(stream)));
+  return KPD_OK;
+}
+
+int kpd_conv1x1(const float* x, int B, int Cin, int HW, const float* w, const float* b, int Cout, float* out,
+                void* stream) {
+  if (B < 0 || Cin <= 0 || HW < 0 || Cout <= 0 || (B > 0 && HW > 0 && (!x || !w || !out)))
+    return fail(KPD_EINVAL, "bad conv1x1 arguments");
+  HIP_TRY(launch_conv1x1_nchw(x, B, Cin, HW, w, b, Cout, out, reinterpret_cast<hipStream_t>(stream)));
   return KPD_OK;
 }
 

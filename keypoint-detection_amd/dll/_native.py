@@ -29,9 +29,13 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
            "kpd_plan_timing", "kpd_plan_timing_stage", "kpd_plan_timing_query", "kpd_plan_set_detector",
            "kpd_bench_conv16",
-           "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics")
+           "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
+           "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
+           "kpd_roi_align", "kpd_conv1x1")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
+HEAD_CHANNEL_ATT, HEAD_SPATIAL_ATT, HEAD_CONVS, HEAD_ALL = 1, 2, 4, 7
+DECODE_ARGMAX, DECODE_SUBPIXEL, DECODE_SOFTARGMAX, DECODE_MODEL = 0, 1, 2, 3
 STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",
           "hm_conv2", "hm_conv3", "hm_final_decode", "keypoint_head")
 
@@ -74,6 +78,19 @@ def load() -> ctypes.CDLL:
     lib.kpd_keypoint_metrics.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_long, ctypes.POINTER(ctypes.c_float),
                                          c_int, c_void_p, c_void_p]
     lib.kpd_nms.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_float, c_int, c_void_p, c_void_p, c_void_p]
+    c_float = ctypes.c_float
+    lib.kpd_heatmap_head.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]
+    lib.kpd_keypoint_head.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]
+    lib.kpd_backbone.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]
+    lib.kpd_channel_attention.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                          c_void_p, c_void_p]
+    lib.kpd_decode_heatmaps.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]
+    lib.kpd_roi_align.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_int,
+                                  c_int, c_void_p, c_void_p]
+    lib.kpd_conv1x1.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
     for name in EXPORTS:
         if name not in ("kpd_last_error", "kpd_version", "kpd_plan_destroy"):
             getattr(lib, name).restype = c_int
@@ -159,6 +176,62 @@ class Plan:
               "kpd_plan_timing_query")
         return ms.value, n.value
 
+    # ---- stand-alone operators (the reference's submodule forwards) ----
+    def heatmap_head(self, x: torch.Tensor, parts: int = HEAD_ALL):
+        """HeatmapHead stages on x [R,64,56,56] -> (heat [R,17,56,56] or None,
+        channel weights [R,64], spatial weights [R,56,56])."""
+        x = _dev_f32(x, "x")
+        R, C, H, W = x.shape
+        if C != 64:
+            raise ValueError(f"HeatmapHead expects 64 input channels, got {C}")
+        heat = torch.empty(R, 17, H, W, device=x.device) if parts & HEAD_CONVS else None
+        cw = torch.empty(R, 64, device=x.device)
+        sw = torch.empty(R, H, W, device=x.device)
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_heatmap_head(self.h, _ptr(x), R, H, W, int(parts), _ptr(heat), _ptr(cw), _ptr(sw),
+                                            _stream(self.device)), "kpd_heatmap_head")
+        return heat, cw, sw
+
+    def keypoint_head(self, x: torch.Tensor):
+        x = _dev_f32(x, "x")
+        R, C, H, W = x.shape
+        if C != 128:
+            raise ValueError(f"KEYPOINT_HEAD path expects 128 input channels, got {C}")
+        kp = torch.empty(R, 17, 2, device=x.device)
+        vis = torch.empty(R, 17, 3, device=x.device)
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_keypoint_head(self.h, _ptr(x), R, H, W, _ptr(kp), _ptr(vis), _stream(self.device)),
+                  "kpd_keypoint_head")
+        return kp, vis
+
+    def backbone(self, image: torch.Tensor):
+        image = _dev_f32(image, "image")
+        B, C, H, W = image.shape
+        h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        sizes = [(h, w)]
+        for k, s_ in ((3, 2), (3, 2), (3, 1), (5, 2), (5, 1), (5, 1), (5, 1), (5, 1), (5, 2), (5, 1), (5, 1)):
+            pd = (k - 1) // 2
+            h, w = (h + 2 * pd - k) // s_ + 1, (w + 2 * pd - k) // s_ + 1
+            sizes.append((h, w))
+        outs = [torch.empty(B, 128, *sizes[i], device=image.device) for i in (0, 3, 8, 11)]
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_backbone(self.h, _ptr(image), B, C, H, W, *[_ptr(o) for o in outs],
+                                        _stream(self.device)), "kpd_backbone")
+        return outs
+
+    def channel_attention(self, x: torch.Tensor, k: int = 64, select: bool = False):
+        """ChannelAttention scores [B,128]; top-k indices [B,k] (int64) and, with
+        select, the gathered channels [B,k,H,W]."""
+        x = _dev_f32(x, "x")
+        B, C, H, W = x.shape
+        scores = torch.empty(B, C, device=x.device)
+        topk = torch.empty(B, k, device=x.device, dtype=torch.int32)
+        sel = torch.empty(B, k, H, W, device=x.device) if select else None
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_channel_attention(self.h, _ptr(x), B, C, H, W, _ptr(scores), _ptr(topk), int(k),
+                                                 _ptr(sel), _stream(self.device)), "kpd_channel_attention")
+        return scores, topk.long(), sel
+
     def debug_buffer(self, name: str) -> torch.Tensor:
         n = ctypes.c_size_t()
         check(self.lib.kpd_debug_copy(self.h, name.encode(), None, 0, ctypes.byref(n), None), "kpd_debug_copy")
@@ -166,6 +239,86 @@ class Plan:
         check(self.lib.kpd_debug_copy(self.h, name.encode(), _ptr(out), n.value, None, _stream(self.device)),
               "kpd_debug_copy")
         return out
+
+
+def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    _require_cuda(t, name)
+    return t.float().contiguous()
+
+
+def decode_heatmaps(heat: torch.Tensor, mode: int, param: float = 0.0):
+    """Heatmap decoders on the device: heat [B,K,H,W] -> keypoints [B,K,2],
+    scores [B,K], vis [B,K,3] (mode DECODE_MODEL; else None)."""
+    heat = _dev_f32(heat, "heatmaps")
+    if heat.dim() != 4:
+        raise ValueError(f"expected [B,K,H,W] heatmaps, got {tuple(heat.shape)}")
+    B, K, H, W = heat.shape
+    kp = torch.empty(B, K, 2, device=heat.device)
+    sc = torch.empty(B, K, device=heat.device)
+    vis = torch.empty(B, K, 3, device=heat.device) if mode == DECODE_MODEL else None
+    lib = load()
+    with torch.cuda.device(heat.device):
+        check(lib.kpd_decode_heatmaps(_ptr(heat), B * K, H, W, int(mode), float(param), _ptr(kp), _ptr(sc), _ptr(vis),
+                                      _stream(heat.device)), "kpd_decode_heatmaps")
+    return kp, sc, vis
+
+
+def roi_align(features: torch.Tensor, rois: torch.Tensor, output_size, spatial_scale: float = 1.0,
+              sampling_ratio: int = -1, aligned: bool = False) -> torch.Tensor:
+    """torchvision.ops.roi_align with a [R,5] (batch index, x1, y1, x2, y2) box tensor."""
+    features = _dev_f32(features, "features")
+    rois = rois.to(features.device, torch.float32).contiguous()
+    if rois.dim() != 2 or rois.size(1) != 5:
+        raise ValueError("rois must be [R, 5]")
+    oh, ow = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
+    B, C, H, W = features.shape
+    out = torch.empty(rois.size(0), C, oh, ow, device=features.device)
+    lib = load()
+    with torch.cuda.device(features.device):
+        check(lib.kpd_roi_align(_ptr(features), B, C, H, W, _ptr(rois), rois.size(0), oh, ow, float(spatial_scale),
+                                int(sampling_ratio), int(bool(aligned)), _ptr(out), _stream(features.device)),
+              "kpd_roi_align")
+    return out
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """nn.Conv2d(k=1) forward on NCHW device tensors."""
+    x = _dev_f32(x, "x")
+    B, C, H, W = x.shape
+    w = weight.detach().to(x.device, torch.float32).reshape(weight.shape[0], -1).contiguous()
+    if w.shape[1] != C:
+        raise ValueError(f"weight expects {w.shape[1]} input channels, got {C}")
+    b = None if bias is None else bias.detach().to(x.device, torch.float32).contiguous()
+    out = torch.empty(B, w.shape[0], H, W, device=x.device)
+    lib = load()
+    with torch.cuda.device(x.device):
+        check(lib.kpd_conv1x1(_ptr(x), B, C, H * W, _ptr(w), _ptr(b), w.shape[0], _ptr(out), _stream(x.device)),
+              "kpd_conv1x1")
+    return out
+
+
+class PlanCache:
+    """A submodule's own plan (its weights registered under the model's
+    state-dict prefix), rebuilt when a parameter changes -- what the model
+    does for its whole-forward plan (keypoint_model.py)."""
+
+    def __init__(self, prefix: str, in_channels: int = 3):
+        self.prefix, self.in_channels = prefix, in_channels
+        self.plan, self.key = None, None
+
+    def get(self, module: torch.nn.Module, device: torch.device, precision: str) -> "Plan":
+        sd = module.state_dict(keep_vars=True)
+        key = (device, precision, tuple((t.data_ptr(), t._version) for t in sd.values()))
+        if self.plan is None or self.key != key:
+            plan = Plan(device, self.in_channels)
+            for name, t in sd.items():
+                if t.is_floating_point():
+                    plan.set_tensor(self.prefix + name, t)
+            plan.finalize(PRECISIONS[precision])
+            self.plan, self.key = plan, key
+        return self.plan
 
 
 def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float, max_output: int = 0) -> torch.Tensor:

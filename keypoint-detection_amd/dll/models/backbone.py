@@ -1,10 +1,12 @@
-"""Backbone parameter containers: MobileNetV3-Small body + LightweightFPN.
+"""Backbone: MobileNetV3-Small body + LightweightFPN.
 
-These modules only *hold* the weights under the reference's state-dict names
-(``backbone.body.features.N...`` from torchvision's mobilenet_v3_small via
-``create_feature_extractor``; ``backbone.fpn.{lateral_convs,fpn_convs}``) so
-that reference checkpoints load unchanged.  The arithmetic runs in the native
-HIP plan (csrc/), which folds BN and repacks to NHWC at load time.
+The modules keep the reference's state-dict names (``backbone.body.features.N...``
+from torchvision's mobilenet_v3_small via ``create_feature_extractor``;
+``backbone.fpn.{lateral_convs,fpn_convs}``) so that reference checkpoints load
+unchanged.  ``MobileNetV3Wrapper.forward`` runs the native HIP plan
+(kpd_backbone: csrc/ folds BN and repacks to NHWC at load time) and returns
+the four FPN levels as the reference does; the body and the FPN are one fused
+path there, so their separate forwards name that entry point.
 
 Reference: dll/models/backbone.py:7-39 (LightweightFPN), :247-264
 (MobileNetV3Wrapper); torchvision mobilenet_v3_small topology restated in
@@ -14,6 +16,7 @@ from typing import List
 
 import torch.nn as nn
 
+from .. import _native
 from ..configs.model_config import BackboneConfig
 
 # (in, kernel, expanded, out, use_se, activation, stride) -- torchvision table
@@ -72,6 +75,10 @@ class InvertedResidual(nn.Module):
 class MobileNetV3SmallBody(nn.Module):
     """features.0..12 of mobilenet_v3_small (the part create_feature_extractor keeps)."""
 
+    def forward(self, x):
+        raise NotImplementedError("the MobileNetV3-Small body runs fused with the FPN in the native plan: "
+                                  "call MobileNetV3Wrapper.forward (model.backbone(x))")
+
     def __init__(self, in_channels: int = 3):
         super().__init__()
         mods: List[nn.Module] = [ConvBN(in_channels, 16, 3, 2)]
@@ -82,6 +89,10 @@ class MobileNetV3SmallBody(nn.Module):
 
 
 class LightweightFPN(nn.Module):
+    def forward(self, features):
+        raise NotImplementedError("the FPN runs fused with the body in the native plan: call "
+                                  "MobileNetV3Wrapper.forward (model.backbone(x))")
+
     def __init__(self, in_channels_list, out_channels):
         super().__init__()
         if not isinstance(in_channels_list, list):
@@ -95,6 +106,7 @@ class LightweightFPN(nn.Module):
 
 
 class MobileNetV3Wrapper(nn.Module):
+    precision = "split"   # FPN level 0 as the fp32-accurate f16 split ("fp32": fp32 MFMA)
     """Same attribute names as the reference wrapper: ``body`` and ``fpn``.
 
     ``weights=MobileNet_V3_Small_Weights.DEFAULT`` is a network download in the
@@ -107,6 +119,18 @@ class MobileNetV3Wrapper(nn.Module):
         self.fpn = LightweightFPN(list(FPN_IN_CHANNELS), out_channels)
         self.attention_module = attention_module
         self.in_channels = config.in_channels
+        self._plans = _native.PlanCache("backbone.", config.in_channels)
+
+    def forward(self, x):
+        """x [B, C, H, W] -> the four FPN outputs [B, 128, h_i, w_i] at strides
+        2 / 8 / 16 / 32 (reference backbone.py:258-264, LightweightFPN :29-39).
+        Eval only (BatchNorm running statistics)."""
+        if self.training:
+            raise NotImplementedError("the backbone runs the eval path only; call .eval()")
+        outs = self._plans.get(self, x.device, self.precision).backbone(x)
+        if self.attention_module:
+            outs[0] = self.attention_module(outs[0])
+        return outs
 
 
 class BACKBONE(nn.Module):

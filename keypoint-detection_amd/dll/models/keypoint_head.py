@@ -1,13 +1,19 @@
-"""KEYPOINT_HEAD parameter container (reference: dll/models/keypoint_head.py:9-90).
+"""KEYPOINT_HEAD (reference: dll/models/keypoint_head.py:9-90).
 
 Submodule names match the reference (``spatial_attention.{0,2}``,
 ``regression_branch.{0,1,2,3,7,8,11}``, ``visibility_branch.{0,1,5,6,9}``,
-``ResidualBlock.{conv1.{0,1},bn1,downsample.{0,1}}``).  Not instantiated by
+``ResidualBlock.{conv1.{0,1},bn1,downsample.{0,1}}``).  ``forward`` runs the
+native HIP path (kpd_keypoint_head: spatial attention, the residual blocks
+and 3x3 convs on MFMA with fused BN / ReLU6 / residual epilogues, pooling,
+both Linear layers as GEMMs, LayerNorm + sigmoid heads) on the module's own
+plan under the ``keypoint_head.`` prefix.  Not instantiated by
 ``MultiPersonKeypointModel`` unless ``dual_head=True`` (the reference never
 wires it in, keypoint_model.py:55-57).
 """
+import torch
 import torch.nn as nn
 
+from .. import _native
 from ..configs.model_config import KeypointHeadConfig
 
 
@@ -23,8 +29,11 @@ class ResidualBlock(nn.Module):
 
 
 class KEYPOINT_HEAD(nn.Module):
+    precision = "split"   # the convs run fp32 in every precision; kept for a uniform plan key
+
     def __init__(self, config: KeypointHeadConfig):
         super().__init__()
+        self._plans = _native.PlanCache("keypoint_head.")
         self.num_keypoints = config.num_keypoints
         c = config.in_channels
         self.height, self.width = config.height, config.width
@@ -45,3 +54,13 @@ class KEYPOINT_HEAD(nn.Module):
             nn.AdaptiveAvgPool2d((4, 4)), nn.Flatten(),
             nn.Linear(vc * 16, 128), nn.LayerNorm(128), nn.ReLU6(inplace=True),
             nn.Dropout(config.dropout_rate), nn.Linear(128, self.num_keypoints * 3))
+
+    def forward(self, x: torch.Tensor):
+        """x [B, 128, 56, 56] -> (keypoints [B, 17, 2], visibility [B, 17, 3]),
+        both sigmoid outputs (reference :50-62).  Eval only (BatchNorm running
+        statistics, dropout off)."""
+        if self.training:
+            raise NotImplementedError("KEYPOINT_HEAD runs the eval path only; call .eval()")
+        if x.dim() != 4 or x.size(2) != self.height or x.size(3) != self.width:
+            raise ValueError(f"expected [B, C, {self.height}, {self.width}] input, got {tuple(x.shape)}")
+        return self._plans.get(self, x.device, self.precision).keypoint_head(x)

@@ -36,7 +36,9 @@ HEATMAP_SIDE = 56
 
 
 class ChannelAttention(nn.Module):
-    """sigmoid(fc(avgpool) + fc(maxpool)), fc = Linear(C, C//16) ReLU Linear (reference :18-44)."""
+    """sigmoid(fc(avgpool) + fc(maxpool)), fc = Linear(C, C//16) ReLU Linear (reference :18-44).
+    ``forward`` runs the native channel statistics + FC kernel (kpd_channel_attention)
+    on the module's own plan (``channel_attention.`` prefix); built for C = 128."""
 
     def __init__(self, in_channels: int, reduction_ratio: int = 16):
         super().__init__()
@@ -44,6 +46,42 @@ class ChannelAttention(nn.Module):
         self.max_pool = nn.AdaptiveMaxPool2d(1)
         red = max(1, in_channels // reduction_ratio)
         self.fc = nn.Sequential(nn.Linear(in_channels, red), nn.ReLU(), nn.Linear(red, in_channels))
+        self._plans = _native.PlanCache("channel_attention.")
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B, C, H, W] -> attention scores [B, C] in (0, 1)."""
+        return self.native_select(x, select=False)[0]
+
+    def native_select(self, x: torch.Tensor, k: int = 64, select: bool = True):
+        """(scores [B, C], top-k channel indices [B, k], x[b, topk[b]] [B, k, H, W] or None)."""
+        return self._plans.get(self, x.device, "fp32").channel_attention(x, k, select)
+
+
+def box_center_to_corners(box: torch.Tensor) -> torch.Tensor:
+    """[cx, cy, w, h] (normalised) -> [x1, y1, x2, y2] clamped to [0, 1] (reference :630-638)."""
+    cx, cy, w, h = box.unbind()
+    return torch.stack([torch.clamp(cx - w / 2, 0, 1), torch.clamp(cy - h / 2, 0, 1),
+                        torch.clamp(cx + w / 2, 0, 1), torch.clamp(cy + h / 2, 0, 1)])
+
+
+def pad_to_length(tensor_list, length):
+    """Truncate / zero-pad a list of tensors to ``length`` (reference :640-651)."""
+    if len(tensor_list) == 0:
+        return []
+    if len(tensor_list) >= length:
+        return tensor_list[:length]
+    template = tensor_list[0]
+    return tensor_list + [torch.zeros_like(template).detach() for _ in range(length - len(tensor_list))]
+
+
+def select_top_k_channels(features: torch.Tensor, channel_attention: nn.Module, k: int = 64) -> torch.Tensor:
+    """features[b, topk(channel_attention(features)[b], k)] -> [B, k, H, W]
+    (reference :653-661): scores, sorted top-k (ties to the lower channel) and
+    the gather in one native call."""
+    if not isinstance(channel_attention, ChannelAttention):
+        raise TypeError("select_top_k_channels runs the native ChannelAttention; pass the model's "
+                        "channel_attention module")
+    return channel_attention.native_select(features, k, select=True)[2]
 
 
 def normalize_bboxes(batch, batch_size: int, device) -> Optional[List[torch.Tensor]]:
@@ -70,14 +108,18 @@ class MultiPersonKeypointModel(nn.Module):
     """Multi-person keypoint detection model (native MI355X inference path).
 
     Extra keyword arguments (not in the reference):
-      precision: "fp32" -- every conv on fp32-input MFMA (exact fp32 products);
+      precision: "split" (default) -- fp32-accurate: FPN level 0 and the
+                 heatmap-head convs as three f16 MFMA products of hi/lo
+                 operand splits (fp32 tolerances: keypoints 1e-5, heatmaps
+                 5e-5, identical top-k / visibility); everything else fp32;
+                 "fp32" -- every conv on fp32-input MFMA (exact fp32 products);
                  "mixed" -- heatmap-head convs on bf16 MFMA with fp32
-                 accumulation; the backbone/FPN feeding the order-critical
-                 channel top-k stays fp32.
+                 accumulation (keypoints within 1e-3); the backbone/FPN feeding
+                 the order-critical channel top-k stays fp32-accurate.
       dual_head: also instantiate KEYPOINT_HEAD (not wired in the reference).
     """
 
-    def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "fp32",
+    def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "split",
                  dual_head: bool = False, max_persons: int = 5, streams: int = 1):
         super().__init__()
         if precision not in _native.PRECISIONS:
@@ -93,7 +135,7 @@ class MultiPersonKeypointModel(nn.Module):
             self.keypoint_head = KEYPOINT_HEAD(config.keypoint_head)
         self.max_persons = max_persons
         self.num_keypoints = config.num_keypoints
-        self.precision = precision
+        self.precision = precision      # (property: also sets the submodules' own plans' precision)
         self.streams = streams          # sub-batch streams for B >= 32 (kpd_plan_set_streams)
         self._plan: Optional[_native.Plan] = None
         self._plan_key = None
@@ -111,7 +153,8 @@ class MultiPersonKeypointModel(nn.Module):
         if self._state_tensors is None:
             self._state_tensors = list(self.state_dict(keep_vars=True).values())
         vers = tuple((t.data_ptr(), t._version) for t in self._state_tensors)
-        return (device, self.precision, self.streams, vers)
+        ph = self.config.person_head
+        return (device, self.precision, self.streams, ph.conf_threshold, ph.nms_iou_threshold, vers)
 
     def _apply(self, fn, *args, **kwargs):
         self._state_tensors = None
@@ -140,13 +183,29 @@ class MultiPersonKeypointModel(nn.Module):
         self._plan, self._plan_key, self._state_tensors = None, None, None
 
     # ------------------------------------------------------------------ forward
+    @property
+    def precision(self) -> str:
+        return self._precision
+
+    @precision.setter
+    def precision(self, value: str) -> None:
+        if value not in _native.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_native.PRECISIONS)}")
+        self._precision = value
+        for m in (self.backbone, self.heatmap_head):
+            m.precision = value
+
     def forward(self, batch) -> Dict[str, torch.Tensor]:
         x = batch["image"] if isinstance(batch, dict) else batch
         if not isinstance(x, torch.Tensor):
             raise TypeError("Input must be a tensor or a dict with 'image' key containing a tensor")
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("training forward/loss is outside the accelerated path; "
-                                      "call model.eval() (inference only)")
+        if self.training:
+            raise NotImplementedError("training mode (batch-statistics BatchNorm, dropout, the loss) is outside "
+                                      "the accelerated inference path; call model.eval()")
+        if isinstance(batch, dict) and "keypoints" in batch and "visibilities" in batch:
+            raise NotImplementedError("a batch with 'keypoints' and 'visibilities' asks for the training loss "
+                                      "and metrics (reference keypoint_model.py:208-209), which are outside the "
+                                      "accelerated inference path; pass only 'image' and 'bboxes'")
         if not x.is_cuda:
             raise _native.KpdNativeError("MultiPersonKeypointModel runs on the HIP device only; "
                                          "move the model input to 'cuda'")
@@ -206,3 +265,34 @@ class MultiPersonKeypointModel(nn.Module):
         if kh_k is not None:
             out["kh_keypoints"], out["kh_visibilities"] = kh_k, kh_v
         return out
+
+    # ------------------------------------------------------------------ helpers (reference :212-313)
+    def extract_roi_features(self, features: torch.Tensor, box: torch.Tensor, output_size=(56, 56)) -> torch.Tensor:
+        """roi_align of one cxcywh box on [1, C, H, W] features -> [1, C, oh, ow]
+        (reference :212-228: corners clamped to [0, 1], scaled to the map,
+        spatial_scale 1, sampling_ratio -1, aligned False)."""
+        B, C, H, W = features.shape
+        corners = box_center_to_corners(box.to(features.device, torch.float32))
+        scale = torch.tensor([W, H, W, H], device=features.device, dtype=torch.float32)
+        rois = torch.cat([torch.zeros(1, device=features.device), corners * scale]).unsqueeze(0)
+        return _native.roi_align(features, rois, output_size)
+
+    def convert_to_original_coords(self, keypoints: torch.Tensor, box) -> torch.Tensor:
+        """ROI-normalised keypoints -> image-normalised, clamped to [0, 1] (reference :230-248)."""
+        shape = keypoints.shape
+        kp = keypoints.view(-1, 2) if keypoints.dim() == 3 else keypoints
+        cx, cy, w, h = box
+        x = torch.clamp(kp[:, 0] * w + (cx - w / 2), 0, 1)
+        y = torch.clamp(kp[:, 1] * h + (cy - h / 2), 0, 1)
+        return torch.stack([x, y], dim=-1).view(shape)
+
+    def decode_heatmap(self, heatmap: torch.Tensor, threshold: float = 0.1):
+        """Soft-argmax keypoints [B, K, 2] and one-hot 3-class visibility
+        [B, K, 3] from sigmoid(max) < 0.3 / < 0.7 / else (reference :250-282);
+        one device kernel (kpd_decode_heatmaps)."""
+        kp, _, vis = _native.decode_heatmaps(heatmap, _native.DECODE_MODEL)
+        return kp, vis
+
+    def _soft_argmax(self, heatmap: torch.Tensor) -> torch.Tensor:
+        """E[x] / (W - 1), E[y] / (H - 1) under softmax over each map (reference :284-313)."""
+        return _native.decode_heatmaps(heatmap, _native.DECODE_SOFTARGMAX, 1.0)[0]

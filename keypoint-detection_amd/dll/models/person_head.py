@@ -60,3 +60,18 @@ class PERSON_HEAD(nn.Module):
         """Greedy NMS (reference :96-139) on the device; returns a CPU int64 index
         tensor like the reference."""
         return _native.nms(boxes, scores, iou_threshold, max_output_size or 0).cpu()
+
+    def forward(self, features, targets=None):
+        """Reference :141-166: with training targets the last FPN level and the
+        target boxes pass through; otherwise every level's box head runs and the
+        last level's prediction [B, 36, h, w] is returned (the reference keeps
+        only that one, so only that one is computed here; kpd_conv1x1)."""
+        if self.training and targets is not None and "bboxes" in targets:
+            return features[-1], targets["bboxes"]
+        # zip(features, box_heads): at most 4 levels; a plain tensor iterates its
+        # batch dim (unbatched [C, h, w] maps), as in the reference
+        feats = list(features)[: len(self.box_heads)]
+        head, x = self.box_heads[len(feats) - 1], feats[-1]
+        if x.dim() == 3:
+            return _native.conv1x1(x.unsqueeze(0), head.weight, head.bias).squeeze(0)
+        return _native.conv1x1(x, head.weight, head.bias)

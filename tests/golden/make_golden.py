@@ -46,11 +46,14 @@ def import_reference():
     import dll.configs as rc  # noqa: F401
     from dll.models.keypoint_model import MultiPersonKeypointModel
     from dll.models.person_head import PERSON_HEAD
-    from dll.models.heatmap_head import HeatmapHead, decode_heatmaps, decode_heatmaps_soft_argmax
+    from dll.models.heatmap_head import (HeatmapHead, decode_heatmaps, decode_heatmaps_soft_argmax,
+                                         decode_heatmaps_subpixel)
     from dll.models.keypoint_head import KEYPOINT_HEAD
+    from dll.models import keypoint_model as km
     return types.SimpleNamespace(cfg=rc, Model=MultiPersonKeypointModel, PersonHead=PERSON_HEAD,
                                  HeatmapHead=HeatmapHead, KeypointHead=KEYPOINT_HEAD,
-                                 decode_heatmaps=decode_heatmaps, decode_sa=decode_heatmaps_soft_argmax)
+                                 decode_heatmaps=decode_heatmaps, decode_sa=decode_heatmaps_soft_argmax,
+                                 decode_sub=decode_heatmaps_subpixel, km=km)
 
 
 def load_synthetic():
@@ -81,9 +84,61 @@ def run_case(m, image, bboxes):
     return feats, scores, out
 
 
+def make_decoders(R, m3):
+    """Heatmap decoders and model helpers on their own inputs (decoders.npz;
+    inputs from decoder_cases.py): random maps, exact ties and a border peak
+    (window clipping), an all-zero map (subpixel: zero mass), [K, H, W] input,
+    non-square maps, and box_center_to_corners / pad_to_length /
+    convert_to_original_coords / ChannelAttention + select_top_k_channels /
+    extract_roi_features."""
+    import decoder_cases
+    c = decoder_cases.inputs()
+    h, hr, kp, feats, boxes = c["h"], c["hr"], c["kp"], c["feats"], c["boxes"]
+    out = {}
+    out["argmax_kpts"], out["argmax_scores"] = [t.numpy() for t in R.decode_heatmaps(h)]
+    for w in (3, 5):
+        k, sc = R.decode_sub(h, window_size=w)
+        out[f"sub{w}_kpts"], out[f"sub{w}_scores"] = k.numpy(), sc.numpy()
+    for i, t in enumerate((1.0, 0.25)):
+        k, sc = R.decode_sa(h, temperature=t)
+        out[f"sa{i}_kpts"], out[f"sa{i}_scores"] = k.numpy(), sc.numpy()
+    out["sa_temps"] = np.array([1.0, 0.25], dtype=np.float32)
+    k3, s3 = R.decode_heatmaps(h[2])                   # [K, H, W] input
+    out["argmax3d_kpts"], out["argmax3d_scores"] = k3.numpy(), s3.numpy()
+    k3, s3 = R.decode_sub(h[2])
+    out["sub3d_kpts"], out["sub3d_scores"] = k3.numpy(), s3.numpy()
+    out["hr_argmax_kpts"] = R.decode_heatmaps(hr)[0].numpy()
+    out["hr_sub_kpts"] = R.decode_sub(hr)[0].numpy()
+    out["hr_sa_kpts"] = R.decode_sa(hr)[0].numpy()
+    with torch.no_grad():
+        mk, mv = m3.decode_heatmap(h)
+        out["model_kpts"], out["model_vis"] = mk.numpy(), mv.numpy()
+        out["model_sa"] = m3._soft_argmax(h).numpy()
+        out["corners"] = torch.stack([R.km.box_center_to_corners(b) for b in boxes]).numpy()
+        out["kp_orig"] = torch.stack([m3.convert_to_original_coords(kp.clone(), b) for b in boxes]).numpy()
+        scores = m3.channel_attention(feats)
+        out["ca_scores"] = scores.numpy()
+        out["ca_topk"] = torch.topk(scores, 64, dim=1).indices.numpy()
+        sel = R.km.select_top_k_channels(feats, m3.channel_attention, k=64)
+        out["selected_sum"] = sel.double().sum(dim=(2, 3)).numpy()
+        roi = m3.extract_roi_features(feats[:1], boxes[1])
+        out["roi_feat_shape"] = np.array(roi.shape)
+        out["roi_feat_slice"] = roi[0, :8, 20:28, 10:18].numpy()
+        out["roi_feat_sum"] = roi.double().sum(dim=(2, 3)).numpy()
+    padded = R.km.pad_to_length([torch.ones(2, 3), 2 * torch.ones(2, 3)], 4)
+    out["padded"] = torch.stack(padded).numpy()
+    np.savez_compressed(OUT / "decoders.npz", **out)
+
+
 def main():
     R = import_reference()
     S = load_synthetic()
+    if "--only-decoders" in sys.argv:
+        torch.manual_seed(0)
+        m3, _ = build_model(R, S, 3)
+        make_decoders(R, m3)
+        print("decoders done")
+        return
     torch.manual_seed(0)
     m3, sd3 = build_model(R, S, 3)
     np.savez_compressed(OUT / "weights_fingerprint.npz",
@@ -167,6 +222,8 @@ def main():
                         heat_sum=hmap.double().sum(dim=(2, 3)).numpy(), heat_slice=hmap[:, :, 20:24, 30:34].numpy(),
                         argmax_kpts=dk.numpy(), argmax_scores=ds.numpy(), sa_kpts=sk.numpy(), sa_scores=ss.numpy(),
                         model_kpts=kk.numpy(), model_vis=kv.numpy(), model_softargmax=ka.numpy())
+
+    make_decoders(R, m3)
 
     # ---- KEYPOINT_HEAD standalone (the 'dual head'); config from the YAML (56x56)
     kcfg = R.cfg.KeypointHeadConfig(height=56, width=56)
