@@ -1023,15 +1023,22 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // CIN: input channels as a compile-time constant (0 = p.cin): the K loop's
 // trip count is then known to the compiler, and conv 1 / conv 2 are separate
 // kernels in a trace
-template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0>
+// TPS (SPLIT only): taps per K-step -- the weights of TPS consecutive taps of
+// a chunk are staged together and one barrier serves all of them (the BN = 64
+// conv 3 has too few MFMAs per tap to amortise a barrier).
+// DB (SPLIT only): double-buffered fragment sets -- step k+1's operands are
+// all read while step k's three passes run (conv 3: few MFMAs per pass and
+// registers to spare; the BN = 256 tiles have no room for a second set).
+template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false>
 __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
   static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
   constexpr int A_LD = AWIN / 8 / 8;                     // A-window DMA wave-instructions per wave (6)
   constexpr int B_LD = BN / 64;                          // B DMA wave-instructions per wave per K-step
-  constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB;
+  constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
   constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
+  static_assert(TPS == 1 || (SPLIT && 9 % TPS == 0), "taps per step");
   constexpr bool FINAL = BN == 64;
   constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BMH, 128, NT>();
   constexpr int LDS = RING > EPI ? RING : EPI;
@@ -1067,11 +1074,15 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / 8) + i * 8) * ROWB);
     glds16(rin, dst, a_off[i] == OOB ? OOB : a_off[i] + c * 128, 0);
   };
-  auto issue_b = [&](int k) {          // B K-step k = (chunk, tap) into stage k % SB
-    const int c = k / 9, t = k - c * 9;
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + wave * (BN / 8) * ROWB);
+  auto issue_b = [&](int k) {          // B of K-step k (TPS taps of one chunk) into stage k % SB
 #pragma unroll
-    for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], t * RB + c * 128);
+    for (int u = 0; u < TPS; ++u) {
+      const int sk = k * TPS + u, c = sk / 9, t = sk - c * 9;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + u * BN * ROWB +
+                                                          wave * (BN / 8) * ROWB);
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], t * RB + c * 128);
+    }
   };
   // Barrier of K-step k: B(k) landed.  A-window pieces are issued before the
   // B of the same batch, so every DMA younger than B(k) is among the
@@ -1082,7 +1093,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   static_assert(SB >= 2 && SB <= 4, "weight ring");
   auto barrier_k = [&](bool tail) {
     if (tail) wait_vmcnt<0>();
-    else wait_vmcnt<(SB - 2) * B_LD>();
+    else wait_vmcnt<(SB - 2) * B_LD * TPS>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1147,23 +1158,37 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   }
   const int rbound = (rlo + 1) * HPP;       // first padded position of the tile's second ROI
   // prologue: chunk 0's window and the first SB-1 K-steps' weights
+  const int KS = KT / TPS;                  // K-steps (barriers)
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) issue_a(0, i);
 #pragma unroll
   for (int k = 0; k < SB - 1; ++k)
-    if (k < KT) issue_b(k);
-  barrier_k(KT < SB - 1);
+    if (k < KS) issue_b(k);
+  barrier_k(KS < SB - 1);
   stamp16(p.stamps, 1);
-  if (NC > 1) issue_a(1, 0);
-  if (SB - 1 < KT) issue_b(SB - 1);
+  // the next chunk's window, spread over this chunk's K-steps: pieces of
+  // K-step k1 (TPS = 1: piece t1 at taps 0-5; else an equal share per step)
+  auto issue_a_at = [&](int k1) {
+    const int s1 = k1 * TPS, c1 = s1 / 9, jj = (s1 - c1 * 9) / TPS;
+    if (c1 + 1 >= NC) return;
+    if constexpr (TPS == 1) {
+      if (jj < A_LD) issue_a(c1 + 1, jj);
+    } else {
+      constexpr int NST = 9 / TPS;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i)
+        if (i >= jj * A_LD / NST && i < (jj + 1) * A_LD / NST) issue_a(c1 + 1, i);
+    }
+  };
+  issue_a_at(0);
+  if (SB - 1 < KS) issue_b(SB - 1);
   // DMA issue at barrier k1 (same schedule in both loops): the next chunk's
-  // window spread over this chunk's taps, and B(k1 + SB - 1) into the stage
-  // of B(k1 - 1), whose fragment reads every wave finished before barrier k1
+  // window pieces, and B(k1 + SB - 1) into the stage of B(k1 - 1), whose
+  // fragment reads every wave finished before barrier k1
   auto issue_at = [&](int k1) {
     if constexpr ((DBG & 2) == 0) {
-      const int c1 = k1 / 9, t1 = k1 - c1 * 9;
-      if (c1 + 1 < NC && t1 < A_LD) issue_a(c1 + 1, t1);
-      if (k1 + SB - 1 < KT) issue_b(k1 + SB - 1);
+      issue_a_at(k1);
+      if (k1 + SB - 1 < KS) issue_b(k1 + SB - 1);
     }
   };
   if constexpr (!SPLIT) {
@@ -1205,8 +1230,8 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) f[i] = *reinterpret_cast<const uint4*>(ab + (r0w + i * 16) * ROWB + ach);
     };
-    auto rd_b = [&](int k, int q, uint4* f) {
-      const char* bb = lds + 2 * ABUF + (k % SB) * BSTAGE;
+    auto rd_b = [&](int k, int q, uint4* f) {   // k: tap sub-step
+      const char* bb = lds + 2 * ABUF + ((k / TPS) % SB) * BSTAGE + (k % TPS) * BN * ROWB;
 #pragma unroll
       for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
     };
@@ -1224,16 +1249,70 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
                                                              acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     };
+    if constexpr (DB) {
+      // Taps unrolled (two chunks per iteration, so the fragment set and the
+      // weight stage of every sub-step are compile-time) with the per-lane A
+      // offsets of the nine taps precomputed: the operand addressing is one
+      // add per read, and every pass's operands were read a whole step ago.
+      static_assert(SB == 2 && 9 % TPS == 0, "DB loop: 2-stage ring");
+      int aoff[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r0w = wm * WM + r16 + 64 + (t / 3 - 1) * HP + (t % 3 - 1);
+        aoff[t] = r0w * ROWB + ((g ^ (r0w & 7)) << 4);   // q = 1 (lo): chunk ^ 4, byte ^ 64
+      }
+      struct Frag { uint4 ah[FM], al[FM], bh[FN], bl[FN]; };
+      auto rd_all = [&](int c, int t, int stage, Frag& f) {
+        const char* ab = lds + (c & 1) * ABUF;
+        const char* bb = lds + 2 * ABUF + stage * BSTAGE + (t % TPS) * BN * ROWB + b_row;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          f.al[i] = *reinterpret_cast<const uint4*>(ab + (aoff[t] ^ 64) + i * 16 * ROWB);
+          f.ah[i] = *reinterpret_cast<const uint4*>(ab + aoff[t] + i * 16 * ROWB);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          f.bh[j] = *reinterpret_cast<const uint4*>(bb + j * 16 * ROWB + bch0);
+          f.bl[j] = *reinterpret_cast<const uint4*>(bb + j * 16 * ROWB + bch1);
+        }
+      };
+      Frag f0, f1;
+      rd_all(0, 0, 0, f0);
+      for (int c = 0; c < NC; c += 2) {   // NC even (host check): c even at the top
+#pragma unroll
+        for (int tt = 0; tt < 18; ++tt) {
+          const int cc = c + tt / 9, t = tt % 9, k = cc * 9 + t;
+          Frag& cur = (tt & 1) ? f1 : f0;
+          Frag& nxt = (tt & 1) ? f0 : f1;
+          pass(cur.al, cur.bh);
+          if (k + 1 < KT) {
+            const int tn = (tt + 1) % 18, cn = c + (tt + 1) / 9;   // next sub-step (chunk cn, tap tn % 9)
+            if ((t + 1) % TPS == 0) {
+              const int k1 = (k + 1) / TPS;
+              barrier_k(k1 + SB - 2 >= KS);
+              issue_at(k1);
+            }
+            // stage of the next sub-step: (its K-step) % 2 = (tn / 9 + (tn % 9) / TPS) % 2 with c even
+            rd_all(cn, tn % 9, ((tn / 9) * (9 / TPS) + (tn % 9) / TPS) & 1, nxt);
+          }
+          pass(cur.ah, cur.bh);
+          pass(cur.ah, cur.bl);
+        }
+      }
+    } else {
     rd_a(0, 1, al);
     rd_b(0, 0, bh);
     rd_a(0, 0, ah);
     rd_b(0, 1, bl);
-    for (int k = 0; k < KT; ++k) {
+    for (int k = 0; k < KT; ++k) {   // tap sub-steps; a barrier where a K-step begins
       const bool more = k + 1 < KT;
       pass(al, bh);
       if (more) {
-        barrier_k(k + SB - 1 >= KT);   // B(k+1) and its chunk's window landed; reads of k retired
-        issue_at(k + 1);
+        if ((k + 1) % TPS == 0) {
+          const int k1 = (k + 1) / TPS;
+          barrier_k(k1 + SB - 2 >= KS);   // B(k1) and its chunk's window landed; reads of k1 - 1 retired
+          issue_at(k1);
+        }
         rd_a(k + 1, 1, al);
       }
       pass(ah, bh);
@@ -1243,6 +1322,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
         rd_a(k + 1, 0, ah);
         rd_b(k + 1, 1, bl);
       }
+    }
     }
   }
   __syncthreads();
@@ -1484,9 +1564,18 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     const int bm = fin || bn != 256 ? BM : bm_env == 224 || bm_env == BM ? bm_env : (cost(224) < cost(BM) ? 224 : BM);
     const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
+    static const int hm_tps = getenv("KPD_HM3_TPS1") ? -1 : 0;   // A/B: conv 3 with one tap per K-step
+    static const bool hm_db = getenv("KPD_HM3_NODB") == nullptr;  // A/B: conv 3 single fragment set
 #define HMK(...) hipLaunchKernelGGL((hmconv_kernel<__VA_ARGS__>), grid, dim3(NT), 0, st, a)
-    if (split) {
-      if (fin && a.cin == 256) HMK(64, 4, 0, BM, true, 256);
+    if (split && dbg) {   // ablations (KPD_HMCONV_DBG=1: no MFMA, 2: no K-loop DMA); wrong results by design
+      if (fin && dbg == 1) HMK(64, 4, 1, BM, true, 256);
+      else if (fin) HMK(64, 4, 2, BM, true, 256);
+      else if (dbg == 1) HMK(256, 2, 1, 224, true, 256);
+      else HMK(256, 2, 2, 224, true, 256);
+    } else if (split) {
+      if (fin && a.cin == 256 && hm_db) HMK(64, 2, 0, BM, true, 256, 3, true);
+      else if (fin && a.cin == 256 && !(hm_tps < 0)) HMK(64, 2, 0, BM, true, 256, 3);
+      else if (fin && a.cin == 256) HMK(64, 4, 0, BM, true, 256);
       else if (fin) HMK(64, 4, 0, BM, true);
       else if (bn == 256 && bm == 224 && a.cin == 64) HMK(256, 2, 0, 224, true, 64);
       else if (bn == 256 && bm == 224 && a.cin == 256) HMK(256, 2, 0, 224, true, 256);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase stamps of the heatmap conv 2 (hmconv_kernel, KPD_STAMPS): per
 workgroup the prologue (chunk 0 window + first weights landed), the K loop and
-the epilogue (stores drained).  GPU only:  KPD_STAMPS=1 python3 tools/stamps_hm2.py"""
+the epilogue (stores drained).  GPU only:  KPD_STAMPS=1 python3 tools/stamps_hm2.py [stamps_hm2|stamps_hm3] [split|mixed]"""
 import os
 import sys
 from pathlib import Path
@@ -19,7 +19,8 @@ def main():
     from dll.models import MultiPersonKeypointModel
     from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
     dev = torch.device("cuda:0")
-    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision="mixed", streams=1)
+    prec = sys.argv[2] if len(sys.argv) > 2 else "split"
+    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=prec, streams=1)
     m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
     m = m.to(dev).eval()
     B = 64
@@ -37,7 +38,7 @@ def main():
     t -= t[:, 0].min()
     start, end = t[:, 0], t[:, 3]
     ph = np.diff(t, axis=1)
-    print(f"wgs={len(st)} span={end.max():.1f}us KT={st[0, 5]} starts p10/p50/p90 {np.percentile(start, 10):.1f}/"
+    print(f"{name} {prec}: wgs={len(st)} span={end.max():.1f}us KT={st[0, 5]} starts p10/p50/p90 {np.percentile(start, 10):.1f}/"
           f"{np.median(start):.1f}/{np.percentile(start, 90):.1f}")
     print("phases med (prologue, K loop, epilogue) = " + " ".join(f"{v:.2f}" for v in np.median(ph, axis=0))
           + f"  K loop per step {np.median(ph[:, 1]) / st[0, 5]:.3f}us  wg med {np.median(end - start):.2f}")
