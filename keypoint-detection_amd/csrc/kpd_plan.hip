@@ -1519,6 +1519,9 @@ static int op_work(kpd_plan* p, int R, int flags, hipStream_t st, Work** w) {
   d.B = 0; d.NB = R; d.P = 1; d.flags = flags;
   if (int rc = ensure_work(p, d, kpd_plan::kOpWs, st)) return rc;
   *w = &p->work[kpd_plan::kOpWs];
+  // the split-K scratch of THIS workspace: the thread's last forward may have
+  // run on another plan, whose workspace can be gone by now
+  g_splitk = (*w)->splitk;
   return KPD_OK;
 }
 
