@@ -790,6 +790,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   for (int s2 = 0; s2 < S; ++s2) issue(s2);
   unsigned nf_off[A_LD], nl_off[A_LD], nmask[A_LD];   // the next tile's rows
   int sb = 0;                                          // ring stage of this tile's K-tile 0
+  unsigned long long mt0 = 0;                          // KPD_STAMPS: shader clock at the K loop's start
   for (int round = 0; L < ntiles; ++round) {
     const int Lnext = tile_at(round + 1);
     const bool has_next = Lnext < ntiles;
@@ -805,6 +806,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
       else wait_vmcnt<(S - 1) * LPT + NST>();
       barrier_lds();
       stamp16(p.stamps, 1, 0, L);
+      mt0 = p.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
       rd_a(sb, 1, fa1); rd_b(sb, 0, fb0); rd_b(sb, 1, fb1); rd_a(sb, 0, fa0);
       // Each K-tile is issued as soon as its stage is free: after barrier
       // kt+1 every wave has read tile kt into registers, so tile kt+S (or,
@@ -846,6 +848,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     barrier_lds();   // every wave's fragment reads of the ring retired: the stage of the last K-tile is free
     stamp16(p.stamps, 2, 0, L);
     stamp16(p.stamps, 5, (unsigned long long)KT, L);
+    if (p.stamps) stamp16(p.stamps, 4, __builtin_amdgcn_s_memtime() - mt0, L);   // K loop in shader cycles
     // this tile's geometry for the epilogue; then the next tile's prologue
     const int e_cls = cls, e_n = n, e_jt = jt, e_ca = ca, e_cb = cb, e_q0 = q0;
     const float e_scale = scale;
@@ -956,10 +959,6 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout,
                                                q < RG && (DBG != 4 || (i | e) == 0) ? o : OOB, 0, 0);
       }
-    if (p.stamps) {   // diagnostic build path: the stores' completion
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      stamp16(p.stamps, 4, 0, L);
-    }
     // the stats exchange region is rewritten by the next tile only after the
     // barriers of its K loop
     L = Lnext;
@@ -1166,6 +1165,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     if (k < KS) issue_b(k);
   barrier_k(KS < SB - 1);
   stamp16(p.stamps, 1);
+  stamp16(p.stamps, 6, __builtin_amdgcn_s_memtime());   // shader clock (K-loop clock rate)
   // the next chunk's window, spread over this chunk's K-steps: pieces of
   // K-step k1 (TPS = 1: piece t1 at taps 0-5; else an equal share per step)
   auto issue_a_at = [&](int k1) {
@@ -1325,6 +1325,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     }
     }
   }
+  stamp16(p.stamps, 7, __builtin_amdgcn_s_memtime());
   __syncthreads();
   stamp16(p.stamps, 2);
 

@@ -1007,7 +1007,8 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
 // the stages (KPD_HEAD_*; a disabled attention uses weights 1); sw_out
 // (nullable) receives the spatial weights [R][56][56].
 static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out, hipStream_t st, int parts,
-                            float* sw_out, unsigned long long* stamps2, unsigned long long* stamps3) {
+                            float* sw_out, unsigned long long* stamps2, unsigned long long* stamps3,
+                            unsigned long long* stamps1 = nullptr) {
   std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
   // split: per-ROI operand bounds, hsc[r] = {max|xs| (written here), max|h1| (conv 1)}
   const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
@@ -1027,7 +1028,7 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
   const HmSplit sp2{w.hsc, p->hm1.bc, p->hm1.bs, 0, p->hm2.bc, p->hm2.bs, 1, -1};
   const HmSplit sp3{w.hsc, p->hm2.bc, p->hm2.bs, 1, 0.f, 0.f, -1, -1};
   std::unique_ptr<Stage> c1(new Stage(p, "hm_conv1", st));
-  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st, nullptr, nullptr, &sp1)) return rc;
+  if (int rc = hm_conv(p, p->hm1, w.xs, R, 64, w.h1, 1, st, nullptr, stamps1, &sp1)) return rc;
   c1.reset();
   std::unique_ptr<Stage> c2(new Stage(p, "hm_conv2", st));
   if (int rc = hm_conv(p, p->hm2, w.h1, R, p->hm1.cout_p, w.h2, 1, st, nullptr, stamps2, &sp2))
@@ -1367,7 +1368,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
   if (int rc = run_heatmap_head(p, w, R, P, heat_out, st, KPD_HEAD_ALL, nullptr,
                                  take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
-                                 take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2)))
+                                 take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
+                                 take_stamps("stamps_hm1", (size_t)(((long)R * 58 * 58 - 116 + 255) / 224) * 2)))
     return rc;
   {
     Stage sg(p, "hm_final_decode", st);

@@ -42,6 +42,9 @@ def main():
           f"{np.median(start):.1f}/{np.percentile(start, 90):.1f}")
     print("phases med (prologue, K loop, epilogue) = " + " ".join(f"{v:.2f}" for v in np.median(ph, axis=0))
           + f"  K loop per step {np.median(ph[:, 1]) / st[0, 5]:.3f}us  wg med {np.median(end - start):.2f}")
+    if (st[:, 7] > st[:, 6]).all():   # shader-clock stamps around the K loop (hmconv)
+        ghz = (st[:, 7] - st[:, 6]).astype(np.float64) / np.maximum(ph[:, 1] * 1e3, 1e-9)
+        print(f"K-loop shader clock GHz p10/p50/p90 {np.percentile(ghz, 10):.3f}/{np.median(ghz):.3f}/{np.percentile(ghz, 90):.3f}")
 
 
 if __name__ == "__main__":
