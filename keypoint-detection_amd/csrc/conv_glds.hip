@@ -790,6 +790,7 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   for (int s2 = 0; s2 < S; ++s2) issue(s2);
   unsigned nf_off[A_LD], nl_off[A_LD], nmask[A_LD];   // the next tile's rows
   int sb = 0;                                          // ring stage of this tile's K-tile 0
+  const bool late = p.stagger && __builtin_amdgcn_readfirstlane(wave) >= 4;   // wave-uniform (see the K loop)
   unsigned long long mt0 = 0;                          // KPD_STAMPS: shader clock at the K loop's start
   for (int round = 0; L < ntiles; ++round) {
     const int Lnext = tile_at(round + 1);
@@ -818,18 +819,28 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         __builtin_amdgcn_s_setprio(1);
         pass(fa1, fb0);
         __builtin_amdgcn_s_setprio(0);
-        if (more) {
-          tile_ready(kt + 1, kt + 2 < KT || has_next, round > 0 && kt + 1 <= 2);
+        // Stagger (KPD_FPN0X_NOSTAGGER: off): waves 0-3 issue this barrier's DMA
+        // pieces right after it, their SIMD partners 4-7 after pass 2, so one
+        // wave of each SIMD pair issues while the other one's MFMAs run
+        // (MI355X_MICROARCH.md "Two waves that run the SAME program").  The
+        // stage written was freed at this barrier; the pieces still precede
+        // the next barrier, so the counted waits are unchanged.
+        auto issue_k = [&]() {
           if (DBG != 2) {
             if (kt + S < KT) issue(is);
             else if (has_next) issue_tap0(is, kt + S - KT, nf_off, nmask);
           }
           is = is + 1 == S ? 0 : is + 1;
+        };
+        if (more) {
+          tile_ready(kt + 1, kt + 2 < KT || has_next, round > 0 && kt + 1 <= 2);
+          if (!late) issue_k();
           rd_a(ns, 1, fa1);
         }
         __builtin_amdgcn_s_setprio(1);
         pass(fa0, fb1);
         __builtin_amdgcn_s_setprio(0);
+        if (more && late) issue_k();
         if (kt == 0 && has_next) {
           rows(Lnext, nf_off, nl_off, nmask);
           nscale = s_unscale[(Lnext >> 4) / p.tpc];
@@ -1235,6 +1246,11 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
     };
+    // stagger (HmConvArgs::stagger): waves 4-7 issue a barrier's DMA pieces
+    // after pass 2 instead of right after the barrier, so one wave of each
+    // SIMD pair issues while its partner's MFMAs run (conv 1 / 2 K step
+    // 1.84 / 1.81 -> 1.75 / 1.77 us)
+    const bool late = p.stagger && __builtin_amdgcn_readfirstlane(wave) >= 4;
     auto pass = [&](const uint4* a, const uint4* b) {
       if constexpr ((DBG & 1) != 0) {
         acc[0][0][0] += __uint_as_float(a[0].x ^ b[FN - 1].w);
@@ -1285,17 +1301,19 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
           Frag& cur = (tt & 1) ? f1 : f0;
           Frag& nxt = (tt & 1) ? f0 : f1;
           pass(cur.al, cur.bh);
+          const bool kstep = k + 1 < KT && (t + 1) % TPS == 0;
           if (k + 1 < KT) {
             const int tn = (tt + 1) % 18, cn = c + (tt + 1) / 9;   // next sub-step (chunk cn, tap tn % 9)
-            if ((t + 1) % TPS == 0) {
+            if (kstep) {
               const int k1 = (k + 1) / TPS;
               barrier_k(k1 + SB - 2 >= KS);
-              issue_at(k1);
+              if (!late) issue_at(k1);
             }
             // stage of the next sub-step: (its K-step) % 2 = (tn / 9 + (tn % 9) / TPS) % 2 with c even
             rd_all(cn, tn % 9, ((tn / 9) * (9 / TPS) + (tn % 9) / TPS) & 1, nxt);
           }
           pass(cur.ah, cur.bh);
+          if (kstep && late) issue_at((k + 1) / TPS);
           pass(cur.ah, cur.bl);
         }
       }
@@ -1305,17 +1323,18 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     rd_a(0, 0, ah);
     rd_b(0, 1, bl);
     for (int k = 0; k < KT; ++k) {   // tap sub-steps; a barrier where a K-step begins
-      const bool more = k + 1 < KT;
+      const bool more = k + 1 < KT, kstep = more && (k + 1) % TPS == 0;
       pass(al, bh);
       if (more) {
-        if ((k + 1) % TPS == 0) {
+        if (kstep) {
           const int k1 = (k + 1) / TPS;
           barrier_k(k1 + SB - 2 >= KS);   // B(k1) and its chunk's window landed; reads of k1 - 1 retired
-          issue_at(k1);
+          if (!late) issue_at(k1);
         }
         rd_a(k + 1, 1, al);
       }
       pass(ah, bh);
+      if (kstep && late) issue_at((k + 1) / TPS);
       if (more) rd_b(k + 1, 0, bh);
       pass(ah, bl);
       if (more) {
@@ -1567,6 +1586,8 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
     static const int hm_tps = getenv("KPD_HM3_TPS1") ? -1 : 0;   // A/B: conv 3 with one tap per K-step
     static const bool hm_db = getenv("KPD_HM3_NODB") == nullptr;  // A/B: conv 3 single fragment set
+    static const bool hm_stagger = getenv("KPD_HM_NOSTAGGER") == nullptr;   // A/B: staggered DMA issue (split)
+    a.stagger = hm_stagger ? 1 : 0;
 #define HMK(...) hipLaunchKernelGGL((hmconv_kernel<__VA_ARGS__>), grid, dim3(NT), 0, st, a)
     if (split && dbg) {   // ablations (KPD_HMCONV_DBG=1: no MFMA, 2: no K-loop DMA); wrong results by design
       if (fin && dbg == 1) HMK(64, 4, 1, BM, true, 256);
@@ -1618,10 +1639,13 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   static const int grid_env = getenv("KPD_FPN0X_GRID") ? atoi(getenv("KPD_FPN0X_GRID")) : 0;   // A/B
   const long grid = std::min<long>(tiles, grid_env > 0 ? grid_env : ncu);
   static const int dbg = getenv("KPD_FPN0X_DBG") ? atoi(getenv("KPD_FPN0X_DBG")) : 0;   // ablations only
-  if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, a);
-  else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, a);
-  else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, a);
+  static const bool stagger = getenv("KPD_FPN0X_NOSTAGGER") == nullptr;                   // A/B
+  Fpn0xArgs b = a;
+  b.stagger = stagger ? 1 : 0;
+  if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, b);
+  else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, b);
+  else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, b);
+  else hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   return hipGetLastError();
 }
 

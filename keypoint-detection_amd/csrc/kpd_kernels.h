@@ -81,6 +81,7 @@ struct HmConvArgs {
   float* heat;
   int r0;                // first ROI of the launch chunk (launcher)
   int in_bytes, wt_bytes;   // launcher
+  int stagger;              // launcher: split K loop, waves 4-7 issue their DMA one pass later
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_hmconv(const HmConvArgs& a, hipStream_t st);
@@ -108,6 +109,7 @@ struct Fpn0xArgs {
   int sc_n;                // images between the two slot arrays (>= N)
   int N, Hf, Wf, rh, rw, tpc, w_exp0, w_expE;
   int f_bytes, l_bytes, w0_bytes, weff_bytes;
+  int stagger;             // launcher: waves 4-7 issue their K-loop DMA one pass later
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
