@@ -99,6 +99,10 @@ def parse():
                     help="sub-batch streams inside one forward (kpd_plan_set_streams); 2 overlaps the sub-batches "
                          "(~4%% more images/s) but then every kernel shares the GPU and its launch time no longer "
                          "describes the kernel")
+    ap.add_argument("--alt-streams", type=int, default=2,
+                    help="N=1: also time the same workload at this many sub-batch streams (labelled "
+                         "'alt_streams'; 0 = skip); the headline stays single-stream so the roofline's launch "
+                         "times describe the kernel alone")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r02" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
@@ -370,6 +374,15 @@ def main():
                        "before the timed region; the dominant stage's figure is its timed-region mean",
         "cpu_baseline": None,
     }
+    if world == 1 and a.alt_streams and a.alt_streams != a.streams and B // 16 >= 2:
+        # the same model, batch and precision as concurrent sub-batches (kpd_plan_set_streams): the
+        # sub-batches' kernels overlap, so this is a throughput figure only (no per-kernel timing)
+        m.streams = a.alt_streams
+        el3, _ = run_steps(m, batch, a.steps, a.warmup, step, False)
+        m.streams = a.streams
+        line["alt_streams"] = {"streams_per_gpu": max(1, min(a.alt_streams, 4, B // 16)),
+                               "value": round(B * a.steps / el3, 2), "ms_per_step": round(el3 / a.steps * 1e3, 4),
+                               "precision": a.precision}
     if world == 1 and a.secondary and a.secondary != a.precision:
         # the same workload at the second precision (labelled; not the headline)
         m2 = build(a.secondary)
