@@ -83,8 +83,9 @@ def flops_per_image(H, W, P, in_ch=3):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed forwards first: the GPU clock ramps over the first ~30 (hm conv 2 0.57 -> 0.51 ms)")
     ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=192)

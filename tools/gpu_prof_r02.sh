@@ -10,7 +10,7 @@ PREC="${PREC:-split}"
 OUTD="$ROOTD/gpurun_out/prof_$PREC"
 mkdir -p "$OUTD"
 cd /tmp && export TMPDIR=/tmp
-BARGS="--steps 6 --warmup 2 --no-cpu-baseline --secondary= --streams 1 --precision $PREC"
+BARGS="--steps 6 --warmup 2 --no-cpu-baseline --secondary= --alt-streams 0 --streams 1 --precision $PREC"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUTD/trace" -o run -- \
   python3 "$ROOTD/bench.py" $BARGS > "$OUTD/trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
 i=0

@@ -68,7 +68,9 @@ def main():
     ap.add_argument("--skip", type=int, default=2)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    res = {"_meta": {"source": a.outdir, "precision": a.precision, "skip_forwards": a.skip}}
+    # repo-relative source path (the GPU box's scratch root differs per call)
+    src = os.path.relpath(os.path.abspath(a.outdir), os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))
+    res = {"_meta": {"source": src, "precision": a.precision, "skip_forwards": a.skip}}
     # ---- kernel trace
     kt = []
     tdir = os.path.join(a.outdir, "trace") if os.path.isdir(os.path.join(a.outdir, "trace")) else a.outdir
@@ -126,7 +128,7 @@ def main():
             if e.get("SQ_VALU_MFMA_BUSY_CYCLES") and e.get("GRBM_GUI_ACTIVE"):
                 e["mfma_busy_frac"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"])
             if ":" in k:
-                e["source"] = a.outdir
+                e["source"] = src
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as fh:
