@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int NTL = p.cout / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = HP + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
+  const int m0 = HP + p.m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
   // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
   // channels as [hi32 | lo32] f16
   const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = 9 * NC;
@@ -1589,6 +1589,32 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     static const bool hm_stagger = getenv("KPD_HM_NOSTAGGER") == nullptr;   // A/B: staggered DMA issue (split)
     a.stagger = hm_stagger ? 1 : 0;
 #define HMK(...) hipLaunchKernelGGL((hmconv_kernel<__VA_ARGS__>), grid, dim3(NT), 0, st, a)
+    // conv 3 (BN 64, one tile per CU round): the rounds after the last full
+    // one would run a partial round of 256-row tiles (64 ROIs: 841 tiles =
+    // 3.3 rounds, the 4th 29 % full).  Instead the full rounds take 256-row
+    // tiles and the rest goes out as 128-row tiles in one extra launch
+    // (146 at 64 ROIs: a half-length round).  Tile sizes never change the
+    // arithmetic of a row (same K order), so results are unchanged.
+    static const bool no_tail = getenv("KPD_HM3_NOTAIL") != nullptr;   // A/B
+    a.m_off = 0;
+    if (fin && !dbg && !no_tail && !a.stamps && (!split || (a.cin == 256 && hm_db))) {
+      const long nfull = rows / BM, F = nfull / ncu * ncu, rem = rows - F * BM, H = (rem + 127) / 128;
+      if (F > 0 && H > 0 && H <= ncu) {
+        const dim3 g1((unsigned)F), g2((unsigned)H);
+        HmConvArgs a2 = a;
+        a2.m_off = (int)(F * BM);
+        if (split) {
+          hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 256, 3, true>), g1, dim3(NT), 0, st, a);
+          hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, 128, true, 256, 3, true>), g2, dim3(NT), 0, st, a2);
+        } else {
+          hipLaunchKernelGGL((hmconv_kernel<64, 4>), g1, dim3(NT), 0, st, a);
+          hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, 128>), g2, dim3(NT), 0, st, a2);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
+      }
+    }
     if (split && dbg) {   // ablations (KPD_HMCONV_DBG=1: no MFMA, 2: no K-loop DMA); wrong results by design
       if (fin && dbg == 1) HMK(64, 4, 1, BM, true, 256);
       else if (fin) HMK(64, 4, 2, BM, true, 256);

@@ -80,6 +80,7 @@ struct HmConvArgs {
   int P;
   float* heat;
   int r0;                // first ROI of the launch chunk (launcher)
+  int m_off;             // launcher: first GEMM row of tile 0 (tail launch of conv 3)
   int in_bytes, wt_bytes;   // launcher
   int stagger;              // launcher: split K loop, waves 4-7 issue their DMA one pass later
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null

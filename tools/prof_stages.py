@@ -9,7 +9,9 @@ forwards (plan setup, warm-up) and everything before the first forward
 (weight upload copies, workspace fills) are dropped, so the numbers describe
 the steady state only.  Kernels are labelled with the plan's stage names:
 fpn0x_kernel -> fpn0; hmconv_kernel<64,...> -> hm_conv3; the first / second
-hmconv_kernel<256|128,...> of a forward -> hm_conv1 / hm_conv2.
+hmconv_kernel<256|128,...> of a forward -> hm_conv1 / hm_conv2.  A stage
+with several launches in one forward (conv 3 and its 128-row tail launch) is
+summed per forward: "per launch" below means per stage execution.
 
 kernel_trace.csv -> mean / min / max duration per stage and per kernel.
 counter_collection.csv (--pmc passes) -> counters averaged per stage; HBM
@@ -83,10 +85,13 @@ def main():
         fw = forwards(kt, key=lambda r: r[0])[a.skip:]
         st, kn = defaultdict(list), defaultdict(list)
         for f in fw:
+            per = defaultdict(float)   # a stage may be several launches (conv 3 + its tail launch): summed
             for (name, us), lab in zip(f, label([n for n, _ in f])):
                 kn[name].append(us)
                 if lab:
-                    st[lab].append(us)
+                    per[lab] += us
+            for lab, us in per.items():
+                st[lab].append(us)
         res["_meta"]["forwards_traced"] = len(fw)
         res["_meta"]["forward_kernel_us"] = round(sum(sum(v) for v in kn.values()) / max(len(fw), 1), 2)
         for lab, v in st.items():
@@ -114,18 +119,22 @@ def main():
         agg = defaultdict(lambda: defaultdict(list))
         for tag, rows in per_tag.items():
             for f in forwards(rows, key=lambda r: r[0])[a.skip:]:
+                per = defaultdict(lambda: defaultdict(float))
                 for (name, cs), lab in zip(f, label([n for n, _ in f])):
                     for c, v in cs.items():
                         if lab:
-                            agg[f"{lab}:{a.precision}"][c].append(v)
+                            per[lab][c] += v
                         agg[name][c].append(v)
+                for lab, cs in per.items():
+                    for c, v in cs.items():
+                        agg[f"{lab}:{a.precision}"][c].append(v)
         for k, cs in agg.items():
             e = res.setdefault(k, {}) if ":" in k else res.setdefault("counters", {}).setdefault(k, {})
             for c, v in cs.items():
                 e[c] = sum(v) / len(v)
             if "FETCH_SIZE" in e or "WRITE_SIZE" in e:
                 e["hbm_bytes_per_launch"] = 2 * e.get("FETCH_SIZE", 0.0) * 1024 + e.get("WRITE_SIZE", 0.0) * 1024
-            if e.get("SQ_VALU_MFMA_BUSY_CYCLES") and e.get("GRBM_GUI_ACTIVE"):
+            if e.get("SQ_VALU_MFMA_BUSY_CYCLES") and e.get("GRBM_GUI_ACTIVE"):   # (a stage's launches summed)
                 e["mfma_busy_frac"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"])
             if ":" in k:
                 e["source"] = src
