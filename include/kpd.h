@@ -161,13 +161,26 @@ int kpd_target_heatmaps(const float* kpts, int planes, int H, int W, float sigma
 int kpd_keypoint_metrics(const float* pred, const float* gt, const float* vis, long n, const float* thresholds,
                          int n_thresholds, float* out, void* stream);
 
+/* Training loss: AdaptiveHeatmapLoss.forward
+ * (dll/losses/keypoint_loss.py:202-280).  pred, gt: [B][K][H][W] fp32,
+ * target_weight: [B][K] or NULL (all device).  Threshold = clamp(torch.quantile(
+ * gt, 0.9), 0.05, 0.3) when adaptive_threshold (radix select on the device,
+ * torch's fp32 rank / lerp), else 0.1.  loss_out (device, 1 float) = mean of
+ * the weighted focal MSE; grad_pred (device [B][K][H][W] or NULL) = d loss /
+ * d pred; threshold_out (device, 1 float, or NULL) = the threshold used.
+ * Deterministic (fixed-order double reductions). */
+int kpd_adaptive_heatmap_loss(const float* pred, const float* gt, const float* target_weight, int B, int K, int H,
+                              int W, float keypoint_weight, float background_weight, int adaptive_threshold,
+                              float focal_alpha, float* loss_out, float* grad_pred, float* threshold_out,
+                              void* stream);
+
 /* Concurrency: a forward pass over B >= 32 images runs as min(n, B/16)
  * contiguous sub-batches on as many streams (forked from / joined back into
  * the caller's stream), so the latency-bound small launches of one sub-batch
  * overlap the other's.  n in [1, 4]; default 1 (n = 2 measured +4% images/s at
  * C2, but every kernel then shares the GPU with the other sub-batch, so
  * per-kernel timings no longer describe the kernel).  Results do not depend
- * on n beyond fp32 rounding in the mixed-precision FPN scale. */
+ * on n: every split-precision scale is per image / per ROI. */
 int kpd_plan_set_streams(kpd_plan* plan, int n);
 
 /* Diagnostics (not part of the reference interface): times the LDS-DMA 3x3

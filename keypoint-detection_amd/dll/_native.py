@@ -31,7 +31,7 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_bench_conv16",
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
            "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
-           "kpd_roi_align", "kpd_conv1x1")
+           "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 HEAD_CHANNEL_ATT, HEAD_SPATIAL_ATT, HEAD_CONVS, HEAD_ALL = 1, 2, 4, 7
@@ -91,6 +91,8 @@ def load() -> ctypes.CDLL:
     lib.kpd_roi_align.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_int,
                                   c_int, c_void_p, c_void_p]
     lib.kpd_conv1x1.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
+    lib.kpd_adaptive_heatmap_loss.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                              c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]
     for name in EXPORTS:
         if name not in ("kpd_last_error", "kpd_version", "kpd_plan_destroy"):
             getattr(lib, name).restype = c_int
@@ -334,3 +336,29 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float, max_out
         check(lib.kpd_nms(_ptr(boxes), _ptr(scores), n, float(iou_threshold), int(max_output or 0), _ptr(keep),
                           _ptr(nk), _stream(boxes.device)), "kpd_nms")
     return keep[: int(nk.item())].long()
+
+
+def adaptive_heatmap_loss(pred: torch.Tensor, gt: torch.Tensor, target_weight: Optional[torch.Tensor],
+                          keypoint_weight: float, background_weight: float, adaptive: bool, focal_alpha: float,
+                          want_grad: bool):
+    """kpd_adaptive_heatmap_loss on [B,K,H,W] fp32 device tensors -> (loss 0-d tensor, grad or None,
+    threshold 0-d tensor)."""
+    for t, n in ((pred, "pred"), (gt, "gt")):
+        _require_cuda(t, n)
+    if pred.dim() != 4 or pred.shape != gt.shape:
+        raise ValueError("AdaptiveHeatmapLoss: pred and gt must be [B, K, H, W] of the same shape")
+    B, K, H, W = pred.shape
+    p = pred.detach().float().contiguous()
+    g = gt.detach().float().contiguous()
+    tw = None
+    if target_weight is not None:
+        _require_cuda(target_weight, "target_weight")
+        tw = target_weight.detach().float().reshape(B, K).contiguous()
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    thr = torch.empty((), dtype=torch.float32, device=pred.device)
+    grad = torch.empty_like(p) if want_grad else None
+    check(load().kpd_adaptive_heatmap_loss(_ptr(p), _ptr(g), _ptr(tw), B, K, H, W, float(keypoint_weight),
+                                           float(background_weight), int(bool(adaptive)), float(focal_alpha),
+                                           _ptr(loss), _ptr(grad), _ptr(thr), _stream(pred.device)),
+          "kpd_adaptive_heatmap_loss")
+    return loss, grad, thr
