@@ -967,8 +967,11 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         const int Y = (int)(((float)q + 0.5f) * inv_rw), X = q - Y * rw;
         const unsigned o =
             (unsigned)((((e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + r16 * 4) * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout,
-                                               q < RG && (DBG != 4 || (i | e) == 0) ? o : OOB, 0, 0);
+        const unsigned so = q < RG && (DBG != 4 || (i | e) == 0) ? o : OOB;
+        // nt: the 403 MB of output streams past the L2 instead of evicting the
+        // weights and the next rounds' input rows (p.out_nt, A/B switch)
+        if (p.out_nt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout, so, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout, so, 0, 0);
       }
     // the stats exchange region is rewritten by the next tile only after the
     // barriers of its K loop
@@ -1668,6 +1671,10 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   static const bool stagger = getenv("KPD_FPN0X_NOSTAGGER") == nullptr;                   // A/B
   Fpn0xArgs b = a;
   b.stagger = stagger ? 1 : 0;
+  // non-temporal output (KPD_FPN0X_NT=0: off): FETCH_SIZE 216 -> 162 MB per launch (the stores no longer
+  // evict the weights and input rows from L2), -1 % time
+  static const int out_nt = getenv("KPD_FPN0X_NT") ? atoi(getenv("KPD_FPN0X_NT")) : 1;
+  b.out_nt = out_nt;
   if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, b);

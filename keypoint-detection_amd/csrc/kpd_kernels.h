@@ -111,6 +111,7 @@ struct Fpn0xArgs {
   int N, Hf, Wf, rh, rw, tpc, w_exp0, w_expE;
   int f_bytes, l_bytes, w0_bytes, weff_bytes;
   int stagger;             // launcher: waves 4-7 issue their K-loop DMA one pass later
+  int out_nt;              // launcher: non-temporal output stores
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
