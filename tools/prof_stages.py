@@ -43,8 +43,14 @@ def label(forward):
         elif k.startswith("hmconv_kernel<64"):
             out.append("hm_conv3")
         elif k.startswith("hmconv_kernel<"):
+            # conv 1 / conv 2 by the compile-time input channels (6th template
+            # argument: 64 / 256; a conv may be two launches), else by order
+            targs = [t.strip() for t in k[len("hmconv_kernel<"):].split(">")[0].split(",")]
             hm += 1
-            out.append("hm_conv1" if hm == 1 else "hm_conv2")
+            if len(targs) >= 6 and targs[5] in ("64", "256"):
+                out.append("hm_conv1" if targs[5] == "64" else "hm_conv2")
+            else:
+                out.append("hm_conv1" if hm == 1 else "hm_conv2")
         else:
             out.append(None)
     return out
