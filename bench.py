@@ -246,12 +246,20 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
                        f"{s} conv3x3 on zero-bordered ROI maps, bf16 operands on v_mfma_f32_16x16x32_bf16")
         else:
             kern[s] = (f, PEAK_TFLOPS["fp32"], f, "conv_mfma_kernel", f"{s} conv3x3 on v_mfma_f32_16x16x4_f32")
+    if precision == "split":
+        kern["hm_conv2"] += ("one stage = two launches: complete rounds of 224-row tiles "
+                             "(hmconv_kernel<256, 2, 0, 224, true, 256>) + the remaining rows as 192-row tiles "
+                             "(hmconv_kernel<256, 2, 0, 192, true, 256>); their rocprofv3 averages sum to avg_ms",)
+    if precision in ("split", "mixed"):
+        kern["hm_conv3"] += ("one stage = two launches: complete rounds of 256-row tiles + the remaining rows as "
+                             "128-row tiles; their rocprofv3 averages sum to avg_ms",)
     cand = [s for s in kern if s in stages]
     if not cand:
         return None
     if dom is None:
         dom = max(cand, key=lambda k: stages[k])
-    flop, peak, exflop, kname, desc = kern[dom]
+    flop, peak, exflop, kname, desc = kern[dom][:5]
+    note = kern[dom][5] if len(kern[dom]) > 5 else None
     t = stages[dom] * 1e-3
     ach, exa = flop / t / 1e12, exflop / t / 1e12
     r = {"bound": "mfma", "kernel": kname, "desc": desc, "stage": dom, "achieved": round(ach, 2), "peak": peak,
@@ -259,6 +267,8 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
          "flop_per_launch": flop, "avg_ms": round(stages[dom], 4),
          "executed_flop_per_launch": exflop, "executed_achieved": round(exa, 2),
          "executed_frac": round(exa / peak, 4)}
+    if note:
+        r["launches_note"] = note
     if exflop > 2.5 * flop:   # 3-product split: each fp32 MAC costs 3 MFMA products
         r["split_ceiling_frac"] = round(ach / (peak / 3.0), 4)
     e = pmc.get(f"{dom}:{precision}") if pmc else None
