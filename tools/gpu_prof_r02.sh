@@ -10,7 +10,7 @@ PREC="${PREC:-split}"
 OUTD="$ROOTD/gpurun_out/prof_$PREC"
 mkdir -p "$OUTD"
 cd /tmp && export TMPDIR=/tmp
-BARGS="--steps 6 --warmup 2 --no-cpu-baseline --secondary= --alt-streams 0 --streams 1 --precision $PREC"
+BARGS="--steps 10 --warmup 40 --no-cpu-baseline --secondary= --alt-streams 0 --streams 1 --precision $PREC"  # past the clock ramp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUTD/trace" -o run -- \
   python3 "$ROOTD/bench.py" $BARGS > "$OUTD/trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
 i=0
@@ -20,4 +20,4 @@ for G in "${PG[@]}"; do
   timeout -k 10 -s KILL 240 rocprofv3 --pmc $G --kernel-trace --output-format csv -d "$OUTD/pmc$i" -o run -- \
     python3 "$ROOTD/bench.py" $BARGS > "$OUTD/pmc$i.log" 2>&1 || { echo "pmc pass $i ($G) rc=$?"; exit 1; }
 done
-python3 "$ROOTD/tools/prof_stages.py" "$OUTD" --precision "$PREC" --skip 2 --out "$OUTD/stages.json"
+python3 "$ROOTD/tools/prof_stages.py" "$OUTD" --precision "$PREC" --skip 42 --out "$OUTD/stages.json"
