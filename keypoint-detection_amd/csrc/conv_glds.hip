@@ -1042,18 +1042,23 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // DB (SPLIT only): double-buffered fragment sets -- step k+1's operands are
 // all read while step k's three passes run (conv 3: few MFMAs per pass and
 // registers to spare; the BN = 256 tiles have no room for a second set).
-template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false>
-__global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
-  constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
+// NW: waves per workgroup (8; 4 for conv 3: 64 x 64 wave tiles, 1.5x fewer
+// LDS fragment bytes per MFMA than 8 waves of 32 x 64, one wave per SIMD).
+template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false,
+          int NW = 8>
+__global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
+  constexpr int NTH = NW * 64;
+  constexpr int WAVES_N = BN / 64, WAVES_M = NW / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
   static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
-  constexpr int A_LD = AWIN / 8 / 8;                     // A-window DMA wave-instructions per wave (6)
-  constexpr int B_LD = BN / 64;                          // B DMA wave-instructions per wave per K-step
+  static_assert(NW == 8 || (BN == 64 && SPLIT && DB), "4 waves: the conv 3 split DB variant only");
+  constexpr int A_LD = AWIN / 8 / NW;                    // A-window DMA wave-instructions per wave (6, NW 4: 12)
+  constexpr int B_LD = BN / 8 / NW;                      // B DMA wave-instructions per wave per K-step
   constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
   constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
   static_assert(TPS == 1 || (SPLIT && 9 % TPS == 0), "taps per step");
   constexpr bool FINAL = BN == 64;
-  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BMH, 128, NT>();
+  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BMH, 128, NTH>();
   constexpr int LDS = RING > EPI ? RING : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -1074,17 +1079,17 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
   unsigned a_off[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int m = m0 - 64 + wave * (AWIN / 8) + i * 8 + lrow;
+    const int m = m0 - 64 + wave * (AWIN / NW) + i * 8 + lrow;
     a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)(m * RB + lchunk * 16) : OOB;
   }
   unsigned b_off[B_LD];
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) {
-    const int co = n0 + wave * (BN / 8) + i * 8 + lrow;
+    const int co = n0 + wave * (BN / NW) + i * 8 + lrow;
     b_off[i] = (unsigned)(co * 9 * RB + lchunk * 16);
   }
   auto issue_a = [&](int c, int i) {   // A window of chunk c, wave-instruction i
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / 8) + i * 8) * ROWB);
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / NW) + i * 8) * ROWB);
     glds16(rin, dst, a_off[i] == OOB ? OOB : a_off[i] + c * 128, 0);
   };
   auto issue_b = [&](int k) {          // B of K-step k (TPS taps of one chunk) into stage k % SB
@@ -1092,7 +1097,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     for (int u = 0; u < TPS; ++u) {
       const int sk = k * TPS + u, c = sk / 9, t = sk - c * 9;
       const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + u * BN * ROWB +
-                                                          wave * (BN / 8) * ROWB);
+                                                          wave * (BN / NW) * ROWB);
 #pragma unroll
       for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], t * RB + c * 128);
     }
@@ -1145,12 +1150,15 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f.a[i]),
                                                             __builtin_bit_cast(bf16x8, f.b[j]), acc[i][j], 0, 0, 0);
   };
-  // fused final layer weights, loaded before the K loop (3 per thread)
-  float fin_pre[3] = {0.f, 0.f, 0.f};
+  // fused final layer weights, loaded before the K loop (3 or 5 per thread)
+  constexpr int FPRE = (17 * 65 + NTH - 1) / NTH;
+  float fin_pre[FPRE];
+#pragma unroll
+  for (int u = 0; u < FPRE; ++u) fin_pre[u] = 0.f;
   if constexpr (FINAL) {
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int i = tid + u * NT;
+    for (int u = 0; u < FPRE; ++u) {
+      const int i = tid + u * NTH;
       if (i < 17 * 64) fin_pre[u] = p.fin_w[i];
       else if (i < 17 * 65) fin_pre[u] = p.fin_b[i - 17 * 64];
     }
@@ -1364,7 +1372,7 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
     // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
     float* tile = reinterpret_cast<float*>(lds);
-    constexpr int P4 = 128 + 4, C4 = 32, RS = NT / C4, IT = BMH / RS;
+    constexpr int P4 = 128 + 4, C4 = 32, RS = NTH / C4, IT = BMH / RS;
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
     float mx[2] = {0.f, 0.f};   // SPLIT: max|out| of the tile's two ROIs (>= 0 after ReLU)
 #pragma unroll
@@ -1422,8 +1430,8 @@ __global__ __launch_bounds__(NT) void hmconv_kernel(const HmConvArgs p) {
     constexpr int NKF = 17;
     float* fw = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int i = tid + u * NT;
+    for (int u = 0; u < FPRE; ++u) {
+      const int i = tid + u * NTH;
       if (i < NKF * 65) fw[i] = fin_pre[u];
     }
     __syncthreads();
@@ -1599,6 +1607,9 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // (146 at 64 ROIs: a half-length round).  Tile sizes never change the
     // arithmetic of a row (same K order), so results are unchanged.
     static const bool no_tail = getenv("KPD_HM3_NOTAIL") != nullptr;   // A/B
+    // A/B (KPD_HM3_NW4=1): conv 3 split as 4 waves of 64 x 64 -- 1.5x fewer LDS
+    // bytes per MFMA, but one wave per SIMD hides no latency: 0.204 vs 0.173 ms
+    static const bool hm3_nw4 = getenv("KPD_HM3_NW4") != nullptr;
     a.m_off = 0;
     if (fin && !dbg && !no_tail && !a.stamps && (!split || (a.cin == 256 && hm_db))) {
       const long nfull = rows / BM, F = nfull / ncu * ncu, rem = rows - F * BM, H = (rem + 127) / 128;
@@ -1606,7 +1617,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
         const dim3 g1((unsigned)F), g2((unsigned)H);
         HmConvArgs a2 = a;
         a2.m_off = (int)(F * BM);
-        if (split) {
+        if (split && hm3_nw4) {
+          hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 256, 3, true, 4>), g1, dim3(256), 0, st, a);
+          hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, 128, true, 256, 3, true, 4>), g2, dim3(256), 0, st, a2);
+        } else if (split) {
           hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 256, 3, true>), g1, dim3(NT), 0, st, a);
           hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, 128, true, 256, 3, true>), g2, dim3(NT), 0, st, a2);
         } else {
@@ -1644,7 +1658,9 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
       else if (dbg == 1) HMK(256, 2, 1, 224, true, 256);
       else HMK(256, 2, 2, 224, true, 256);
     } else if (split) {
-      if (fin && a.cin == 256 && hm_db) HMK(64, 2, 0, BM, true, 256, 3, true);
+      if (fin && a.cin == 256 && hm_db && hm3_nw4)
+        hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 256, 3, true, 4>), grid, dim3(256), 0, st, a);
+      else if (fin && a.cin == 256 && hm_db) HMK(64, 2, 0, BM, true, 256, 3, true);
       else if (fin && a.cin == 256 && !(hm_tps < 0)) HMK(64, 2, 0, BM, true, 256, 3);
       else if (fin && a.cin == 256) HMK(64, 4, 0, BM, true, 256);
       else if (fin) HMK(64, 4, 0, BM, true);
