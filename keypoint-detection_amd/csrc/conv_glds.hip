@@ -1592,7 +1592,14 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     }
     static const int bm_env = getenv("KPD_HMCONV_BM") ? atoi(getenv("KPD_HMCONV_BM")) : 0;   // A/B
     auto cost = [&](long bm) { return ((rows + bm - 1) / bm * (a.cout / bn) + ncu - 1) / ncu * bm; };
-    const int bm = fin || bn != 256 ? BM : bm_env == 224 || bm_env == BM ? bm_env : (cost(224) < cost(BM) ? 224 : BM);
+    // conv 1 / 2 (cin 64 / 256) always take 224-row tiles: those are the
+    // instances with the input channels as a compile-time constant (the
+    // generic runtime-cin kernel ran conv 1 + 2 at 640 ROIs (C3) ~2x slower),
+    // and conv 2's tail launch packs the last round
+    const bool spec = a.cin == 64 || a.cin == 256;
+    const int bm = fin || bn != 256 ? BM
+                   : bm_env == 224 || bm_env == BM ? bm_env
+                   : (spec || cost(224) < cost(BM)) ? 224 : BM;
     const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
     static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
     static const int hm_tps = getenv("KPD_HM3_TPS1") ? -1 : 0;   // A/B: conv 3 with one tap per K-step

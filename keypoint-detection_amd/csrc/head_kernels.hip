@@ -151,11 +151,13 @@ __global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, in
 // Also emits per-(roi,row) channel sum/max partials for HeatmapHead attention.
 // CW = channels per lane: 1 -> the 64 top-k channels (HeatmapHead input),
 // 2 -> all 128 FPN channels in order (KEYPOINT_HEAD input, topk == nullptr).
+constexpr int kRoiStageFloats = 12800;   // 50 KB (4 rows x 50 columns of the 64 selected channels): 3 workgroups per CU
 template <int CW>
 __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
                                                         const int32_t* __restrict__ topk,
                                                         const float* __restrict__ boxes, int P,
-                                                        float* __restrict__ roi, float* __restrict__ roi_stats) {
+                                                        float* __restrict__ roi, float* __restrict__ roi_stats,
+                                                        int stage_cap) {
   __shared__ float red[4][2][TOPK];
   constexpr int CO = TOPK * CW;
   const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
@@ -171,9 +173,6 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   const int gw = (int)ceilf(roi_w / (float)HM), gh = (int)ceilf(roi_h / (float)HM);
   const float count = (float)max(gw * gh, 1);
   const float* fb = feat + (size_t)b * Hf * Wf * Cf;
-  int ch[CW];
-#pragma unroll
-  for (int q = 0; q < CW; ++q) ch[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
 
   // The wave's 14 bins (pw = wave + 4 j) advance together through the
   // sampling grid: for each (iy, ix) the 4 corner loads of all 14 bins are
@@ -187,6 +186,85 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   for (int j = 0; j < NB; ++j)
 #pragma unroll
     for (int q = 0; q < CW; ++q) acc[j][q] = 0.f;
+  // Staged path (CW == 1): the output row's source pixels -- rows [ylo, yhi] x
+  // columns [xlo, xhi], every selected channel -- are gathered into LDS once
+  // (each element read from L2 once, instead of once per sample corner: ~4x
+  // fewer L2 bytes), then the samples read LDS.  Same sample positions,
+  // weights and summation order as the direct path; ROIs whose footprint
+  // exceeds the stage fall back to the direct gathers.
+  auto sample_y = [&](int iy, bool& yin, int& yl, int& yh, float& ly, float& hy) {
+    const float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
+    yin = !(y < -1.f || y > (float)Hf);
+    float yy = y <= 0.f ? 0.f : y;
+    yl = (int)yy;
+    if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
+    ly = yy - (float)yl;
+    hy = 1.f - ly;
+  };
+  auto sample_x = [&](int pw, int ix, int& xl, int& xh, float& lx, float& hx, bool& xin) {
+    const float x = x1 + (float)pw * bin_w + ((float)ix + 0.5f) * bin_w / (float)gw;
+    xin = !(x < -1.f || x > (float)Wf);
+    float xx = x <= 0.f ? 0.f : x;
+    xl = (int)xx;
+    if (xl >= Wf - 1) { xh = xl = Wf - 1; xx = (float)xl; } else xh = xl + 1;
+    lx = xx - (float)xl;
+    hx = 1.f - lx;
+  };
+  bool staged = false;
+  int ylo = 0, xlo = 0, nc = 0;
+  if constexpr (CW == 1) {
+    bool t0;
+    int a0, a1, yhi, xhi, d0;
+    float f0, f1;
+    sample_y(0, t0, ylo, a1, f0, f1);
+    sample_y(gh - 1, t0, a0, yhi, f0, f1);
+    sample_x(0, 0, xlo, d0, f0, f1, t0);
+    sample_x(HM - 1, gw - 1, a0, xhi, f0, f1, t0);
+    const int nr = yhi - ylo + 1;
+    nc = xhi - xlo + 1;
+    staged = nr > 0 && nc > 0 && nr * nc * CO <= stage_cap;   // stage_cap: the launch's dynamic LDS (floats)
+    if (staged) {
+      extern __shared__ float stage[];
+      const int chl = topk[b * TOPK + lane];
+      // a wave fills whole pixels: lane = channel (the top-k gather, 4 lines per instruction as before)
+      for (int px = wave; px < nr * nc; px += 4) {
+        const int ry = px / nc, cx2 = px - ry * nc;
+        stage[px * CO + lane] = fb[((size_t)(ylo + ry) * Wf + xlo + cx2) * Cf + chl];
+      }
+      __syncthreads();
+      for (int iy = 0; iy < gh; ++iy) {
+        bool yin;
+        int yl, yh;
+        float ly, hy;
+        sample_y(iy, yin, yl, yh, ly, hy);
+        const int r1 = (yl - ylo) * nc, r2 = (yh - ylo) * nc;
+        for (int ix = 0; ix < gw; ++ix) {
+          float v[NB][4], wgt[NB][4];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            int xl, xh;
+            float lx, hx;
+            bool xin;
+            sample_x(wave + 4 * j, ix, xl, xh, lx, hx, xin);
+            const bool in = yin && xin;
+            wgt[j][0] = in ? hy * hx : 0.f; wgt[j][1] = in ? hy * lx : 0.f;
+            wgt[j][2] = in ? ly * hx : 0.f; wgt[j][3] = in ? ly * lx : 0.f;
+            v[j][0] = stage[(r1 + xl - xlo) * CO + lane];
+            v[j][1] = stage[(r1 + xh - xlo) * CO + lane];
+            v[j][2] = stage[(r2 + xl - xlo) * CO + lane];
+            v[j][3] = stage[(r2 + xh - xlo) * CO + lane];
+          }
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            acc[j][0] += wgt[j][0] * v[j][0] + wgt[j][1] * v[j][1] + wgt[j][2] * v[j][2] + wgt[j][3] * v[j][3];
+        }
+      }
+    }
+  }
+  if (!staged) {
+  int ch[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) ch[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
   for (int iy = 0; iy < gh; ++iy) {
     float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
     const bool yin = !(y < -1.f || y > (float)Hf);
@@ -223,6 +301,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
           acc[j][q] += wgt[j][0] * v[j][0][q] + wgt[j][1] * v[j][1][q] + wgt[j][2] * v[j][2][q] +
                        wgt[j][3] * v[j][3][q];
     }
+  }
   }
   float s_sum = 0.f, s_max = -INFINITY;
 #pragma unroll
@@ -541,12 +620,14 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipSt
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk, const float* boxes,
                             int R, int P, float* roi, float* roi_stats, hipStream_t st) {
   if (topk) {
-    hipLaunchKernelGGL((roi_align_kernel<1>), dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, topk, boxes, P, roi,
-                       roi_stats);
+    static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
+    const int cap = direct ? 0 : kRoiStageFloats;
+    hipLaunchKernelGGL((roi_align_kernel<1>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, topk, boxes, P,
+                       roi, roi_stats, cap);
   } else {
     if (Cf != 2 * TOPK) return hipErrorInvalidValue;
     hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
-                       roi, nullptr);
+                       roi, nullptr, 0);
   }
   return hipGetLastError();
 }
