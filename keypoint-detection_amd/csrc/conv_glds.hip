@@ -1660,8 +1660,8 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
       }
     }
     if (split && dbg) {   // ablations (KPD_HMCONV_DBG=1: no MFMA, 2: no K-loop DMA); wrong results by design
-      if (fin && dbg == 1) HMK(64, 4, 1, BM, true, 256);
-      else if (fin) HMK(64, 4, 2, BM, true, 256);
+      if (fin && dbg == 1) HMK(64, 2, 1, BM, true, 256, 3, true);   // the production conv 3 variant
+      else if (fin) HMK(64, 2, 2, BM, true, 256, 3, true);
       else if (dbg == 1) HMK(256, 2, 1, 224, true, 256);
       else HMK(256, 2, 2, 224, true, 256);
     } else if (split) {
