@@ -80,7 +80,7 @@ def flops_per_image(H, W, P, in_ch=3):
             "hm_conv3": hm_convs[2] * P}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -104,9 +104,13 @@ def parse():
                     help="N=1: also time the same workload at this many sub-batch streams (labelled "
                          "'alt_streams'; 0 = skip); the headline stays single-stream so the roofline's launch "
                          "times describe the kernel alone")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r02" / "pmc.json"),
-                    help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run")
-    return ap.parse_args()
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r03" / "pmc.json"),
+                    help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run (entries are "
+                         "stamped with the hash of the kernel sources they were measured on)")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="test mode: no GPU; gloo ranks on the CPU run a stand-in forward through the same "
+                         "launcher, barrier, timing and collation code (tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
 
 
 def host_cpu_info():
@@ -173,23 +177,115 @@ def cpu_baseline(sd, img, boxes, threads, warmups=3, runs=5, max_seconds=40.0):
                                      "min_s": round(ts[0], 4), "max_s": round(ts[-1], 4)}
 
 
-def run_steps(m, batch, steps, warmup, step_fn, dist):
+def _cuda_sync():
+    torch.cuda.synchronize()
+
+
+def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync):
     """W untimed + K timed steps bracketed by barrier + synchronize; seconds."""
     import torch.distributed as tdist
     with torch.no_grad():
         for _ in range(warmup):
             step_fn()
-        torch.cuda.synchronize()
+        sync()
         if dist:
             tdist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             out = step_fn()
-        torch.cuda.synchronize()
+        sync()
         if dist:
             tdist.barrier()
         return time.perf_counter() - t0, out
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) without a launcher: start N ranks (one per GPU) through
+    torch.distributed.run as a child process and return its exit code.  This
+    process never touches the GPU (no HIP call before or after), and rank 0 of
+    the children prints the JSON line on the inherited stdout."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this host driver (RCCL)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve())] + argv
+    return subprocess.run(cmd, env=env).returncode
+
+
+class StandinModel:
+    """--cpu-standin: a cheap deterministic forward with the drop-in's output
+    contract ([n,P,1,17,2] keypoints, [n,P,1,17,3] one-hot visibilities,
+    [n,P,17,56,56] heatmaps), so the launcher / timing / collation code runs
+    without a GPU.  It is not the model and never produces a bench number."""
+    num_keypoints = 17
+
+    def __call__(self, batch):
+        img, boxes = batch["image"], batch["bboxes"]
+        n, p = boxes.shape[:2]
+        m = img.mean(dim=(1, 2, 3))
+        k = (boxes[..., :2].unsqueeze(2) + 0.01 * m.view(n, 1, 1, 1)).expand(n, p, 17, 2).clamp(0, 1)
+        v = torch.zeros(n, p, 17, 3)
+        v[..., 2] = 1.0
+        return {"keypoints": k.unsqueeze(2).contiguous(), "visibilities": v.unsqueeze(2),
+                "heatmap": torch.zeros(n, p, 17, 56, 56)}
+
+
+def main_standin(a, world, rank, dist):
+    """The N-rank code path of main() with gloo on the CPU and StandinModel."""
+    import torch.distributed as tdist
+    from dll.distributed import collate_outputs
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    torch.set_num_threads(1)
+    B, P = a.batch, a.persons
+    img = synthetic_images(B, 3, a.height, a.width, seed=1234 + 7919 * rank)
+    boxes = synthetic_boxes(B, P, seed=1235 + 7919 * rank)
+    batch = {"image": img, "bboxes": boxes}
+    model = StandinModel()
+    gather = dist and not a.no_gather
+    coll = {}
+
+    def step():
+        out = model(batch)
+        if gather:
+            coll.update(collate_outputs(out, B * world, max_persons=P))
+        return out
+
+    el, _ = run_steps(a.steps, a.warmup, step, dist, sync=lambda: None)
+    per_rank = gather_elapsed(el, world, dist, torch.device("cpu"))
+    el = max(per_rank)
+    line = {"metric": "cpu-standin (launcher test; not a measurement)", "value": round(B * world * a.steps / el, 2),
+            "unit": "images/s", "n_gpus": world, "world": world, "backend": "gloo" if dist else None,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4),
+            "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+            "collated": {k: list(v.shape) for k, v in coll.items()}}
+    if gather:   # every rank's slab landed at its shard's offset
+        from dll.distributed import shard_range
+        line["collated_ok"] = bool(all(
+            torch.equal(coll["visibilities"][s:e, :, 0, :, 2], torch.ones(e - s, P, 17))
+            for s, e in (shard_range(B * world, world, r) for r in range(world))))
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+def gather_elapsed(el, world, dist, dev):
+    """Every rank's elapsed seconds (all_gather; the job time is their max)."""
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if not dist:
+        return [el]
+    import torch.distributed as tdist
+    parts = [torch.empty_like(t) for _ in range(world)]
+    tdist.all_gather(parts, t)
+    return [float(x.item()) for x in parts]
 
 
 def stage_pass(m, plan, batch, iters):
@@ -279,15 +375,43 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
             # MFMA-busy cycles summed over the 1024 SIMDs / (GUI-active cycles per XCD)
             r["mfma_busy_frac"] = round(e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"]), 4)
         r["pmc_source"] = e.get("source")
+        cur = kernel_src_hash()
+        r["pmc_src_hash"] = e.get("src_hash")
+        # the counters were measured on these kernel sources: false = stale (kernel changed since)
+        r["pmc_current"] = e.get("src_hash") == cur
     return r
 
 
-def main():
-    a = parse()
+def kernel_src_hash():
+    """sha256 (16 hex) over the HIP sources + headers libkpd.so is built from;
+    profiles/*/pmc.json entries carry the hash they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    cs = ROOT / "keypoint-detection_amd" / "csrc"
+    for f in sorted(list(cs.glob("*.hip")) + list(cs.glob("*.h")) + [ROOT / "include" / "kpd.h"]):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if a.cpu_standin:
+        if dist:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+        return main_standin(a, world, rank, dist)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist:
@@ -334,16 +458,14 @@ def main():
     mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
     dom = max((k for k in breakdown if k in mfma_stages), key=lambda k: breakdown[k][0], default=None)
     plan.timing(True, stage=dom)
-    el, out = run_steps(m, batch, a.steps, 0, step, dist)
+    el, out = run_steps(a.steps, 0, step, dist)
     plan.timing(False)
     dms, dn = plan.timing_query(dom) if dom else (0.0, 0)
     stages = {k: v[0] for k, v in breakdown.items()}
     if dn:
         stages[dom] = dms / dn
-    el_t = torch.tensor([el], device=dev, dtype=torch.float64)
-    if dist:
-        tdist.all_reduce(el_t, op=tdist.ReduceOp.MAX)
-    el = float(el_t.item())
+    per_rank = gather_elapsed(el, world, dist, dev)
+    el = max(per_rank)
 
     fl = flops_per_image(a.height, a.width, P)
     pmc = None
@@ -355,6 +477,7 @@ def main():
             pmc = None
     roof = roofline(a.precision, stages, fl, Bl, a.height, a.width, pmc, dom)
     if roof:
+        roof["forwards_before_timed"] = a.warmup + 1     # --warmup + the one stage-breakdown forward
         roof["launches_timed"] = dn
         roof["images_per_launch"] = Bl
         roof["timing"] = ("HIP events around every launch of this kernel inside the timed region, on the "
@@ -366,9 +489,11 @@ def main():
               "mixed": ("bf16", "heatmap-head convs bf16 x bf16 (fp32 accumulate); backbone/FPN fp32-accurate")}
     line = {
         "metric": "images/sec @ 256x192 COCO-17 (MultiPersonKeypointModel.forward, given boxes)",
-        "value": round(total_imgs / el, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+        "value": round(total_imgs / el, 2), "unit": "images/s", "n_gpus": world, "world": world,
+        "backend": "nccl (RCCL)" if dist else None, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
+        "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
         "dtype": dtypes[a.precision][0], "dtype_detail": dtypes[a.precision][1],
         "data": "synthetic (seeded U[0,1) images ImageNet-normalised, seeded boxes, seed-0 random weights)",
         "config": {"workload": f"C2: batch {B}/GPU, {a.height}x{a.width}x3, {P} box/img, heatmap head + "
@@ -389,7 +514,7 @@ def main():
         # the same model, batch and precision as concurrent sub-batches (kpd_plan_set_streams): the
         # sub-batches' kernels overlap, so this is a throughput figure only (no per-kernel timing)
         m.streams = a.alt_streams
-        el3, _ = run_steps(m, batch, a.steps, a.warmup, step, False)
+        el3, _ = run_steps(a.steps, a.warmup, step, False)
         m.streams = a.streams
         line["alt_streams"] = {"streams_per_gpu": max(1, min(a.alt_streams, 4, B // 16)),
                                "value": round(B * a.steps / el3, 2), "ms_per_step": round(el3 / a.steps * 1e3, 4),
@@ -404,7 +529,7 @@ def main():
         bd2 = stage_pass(m2, p2, batch, 1)
         d2 = max((k for k in bd2 if k in mfma_stages), key=lambda k: bd2[k][0], default=None)
         p2.timing(True, stage=d2)
-        el2, _ = run_steps(m2, batch, a.steps, 0, lambda: step(m2), False)
+        el2, _ = run_steps(a.steps, 0, lambda: step(m2), False)
         p2.timing(False)
         st2 = {k: v[0] for k, v in bd2.items()}
         if d2:
