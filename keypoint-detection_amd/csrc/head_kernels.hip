@@ -333,7 +333,8 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
 __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__ roi_stats,
                                                        const float* __restrict__ w0, const float* __restrict__ b0,
                                                        const float* __restrict__ w2, const float* __restrict__ b2,
-                                                       float* __restrict__ cw, float* __restrict__ hsc) {
+                                                       float* __restrict__ cw, float* __restrict__ hsc,
+                                                       int abs_in) {
   __shared__ float avg[TOPK], mx[TOPK], h[8];
   const int r = blockIdx.x, c = threadIdx.x;
   const float* st = roi_stats + (size_t)r * HM * 2 * TOPK;
@@ -345,9 +346,10 @@ __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__
   avg[c] = s / (float)HMP;
   mx[c] = m;
   if (hsc) {   // split heatmap convs: U0 = max of the ROI features bounds |xs| (sigmoid gates <= 1)
-    const float u0 = wave_max(m);
+    float u0 = fmaxf(wave_max(m), 0.f);
+    if (abs_in) u0 = fmaxf(u0, hsc[(size_t)r * 4 + 2]);   // features of either sign: max |x|
     if (c == 0) {
-      hsc[(size_t)r * 4] = fmaxf(u0, 0.f);
+      hsc[(size_t)r * 4] = u0;
       hsc[(size_t)r * 4 + 1] = 0.f;   // max|h1|, published by heatmap conv 1
     }
   }
@@ -593,7 +595,8 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
       kpts_out[(o + k) * 2 + 0] = px;
       kpts_out[(o + k) * 2 + 1] = py;
       const float conf = kpd_sigmoid(m);
-      const int cls = conf < 0.3f ? 0 : (conf < 0.7f ? 1 : 2);
+      // compared as the reference does: conf.item() (a double) against 0.3 / 0.7
+      const int cls = (double)conf < 0.3 ? 0 : ((double)conf < 0.7 ? 1 : 2);
       vis_out[(o + k) * 3 + 0] = cls == 0 ? 1.f : 0.f;
       vis_out[(o + k) * 3 + 1] = cls == 1 ? 1.f : 0.f;
       vis_out[(o + k) * 3 + 2] = cls == 2 ? 1.f : 0.f;
@@ -632,8 +635,8 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
   return hipGetLastError();
 }
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,
-                            const float* b2, float* cw, float* hsc, hipStream_t st) {
-  hipLaunchKernelGGL(hm_chattn_kernel, dim3(R), dim3(64), 0, st, roi_stats, w0, b0, w2, b2, cw, hsc);
+                            const float* b2, float* cw, float* hsc, hipStream_t st, int abs_in) {
+  hipLaunchKernelGGL(hm_chattn_kernel, dim3(R), dim3(64), 0, st, roi_stats, w0, b0, w2, b2, cw, hsc, abs_in);
   return hipGetLastError();
 }
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st) {

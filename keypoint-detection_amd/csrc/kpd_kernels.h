@@ -218,9 +218,12 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
                             const float* boxes, int R, int P, float* roi, float* roi_stats,
                             hipStream_t st);
 // hsc != null (split heatmap convs): writes hsc[r][0] = max of ROI r's
-// features (the bound of |xs|) and zeroes hsc[r][1]
+// features (the bound of |xs|: the model's ROI features follow a ReLU) and
+// zeroes hsc[r][1]; abs_in = 1: the features may be negative, hsc[r][2]
+// holds their max |x| (launch_nchw_rows_to_nhwc) and joins the bound
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0,
-                            const float* w2, const float* b2, float* cw, float* hsc, hipStream_t st);
+                            const float* w2, const float* b2, float* cw, float* hsc, hipStream_t st,
+                            int abs_in = 0);
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st);
 // use_sp = 0: no spatial attention (weights 1); sw_out != null: the spatial
 // weights [R][56][56] (HeatmapHead.forward's attention_weights[1])
@@ -264,7 +267,7 @@ hipError_t launch_decode_planes(const float* heat, int planes, int H, int W, int
 hipError_t launch_roi_align_nchw(const float* feat, int C, int H, int W, const float* rois, int R, int oh, int ow,
                                  float scale, int sr, int aligned, float* out, hipStream_t st);
 hipError_t launch_nchw_rows_to_nhwc(const float* in, int N, int C, int H, int W, float* out, float* stats,
-                                    hipStream_t st);
+                                    hipStream_t st, float* amax = nullptr, int amax_stride = 0);
 hipError_t launch_nhwc_to_nchw(const float* in, int N, int HW, int C, float* out, hipStream_t st);
 hipError_t launch_nchw_channel_stats(const float* x, int N, int C, int HW, float* stats, hipStream_t st);
 hipError_t launch_gather_planes(const float* x, int N, int C, int HW, const int32_t* idx, int K, float* out,

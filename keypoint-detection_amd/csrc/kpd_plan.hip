@@ -983,6 +983,9 @@ static bool fpn0x_ok(const kpd_plan* p, const Dims& d) {
 
 static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   if (p->have_work[k] && d.fits(p->dims[k])) return KPD_OK;
+  // re-carving (a larger shape) rewrites and re-zeroes the buffers: let every
+  // earlier use of this workspace, on whichever stream, finish first (rare)
+  if (p->have_work[k]) HIP_TRY(hipDeviceSynchronize());
   Work w;
   const size_t need = carve(p, d, nullptr, w);
   if (need > p->ws_bytes[k]) {
@@ -1008,12 +1011,12 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
 // (nullable) receives the spatial weights [R][56][56].
 static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out, hipStream_t st, int parts,
                             float* sw_out, unsigned long long* stamps2, unsigned long long* stamps3,
-                            unsigned long long* stamps1 = nullptr) {
+                            unsigned long long* stamps1 = nullptr, int abs_in = 0) {
   std::unique_ptr<Stage> att_stage(new Stage(p, "hm_attention", st));
   // split: per-ROI operand bounds, hsc[r] = {max|xs| (written here), max|h1| (conv 1)}
   const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
   HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw,
-                           hsplit ? w.hsc : nullptr, st));
+                           hsplit ? w.hsc : nullptr, st, abs_in));
   if (!(parts & KPD_HEAD_CHANNEL_ATT)) HIP_TRY(launch_fill(w.cw, (long)R * 64, 1.f, st));
   HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
   const bool bf = p->precision == KPD_PRECISION_MIXED;
@@ -1518,7 +1521,9 @@ int kpd_debug_copy(kpd_plan* p, const char* name, void* dst, size_t bytes, size_
 
 static int op_work(kpd_plan* p, int R, int flags, hipStream_t st, Work** w) {
   Dims d;
-  d.B = 0; d.NB = R; d.P = 1; d.flags = flags;
+  // one carve serves both stand-alone heads: the union of their flags, so
+  // alternating HeatmapHead / KEYPOINT_HEAD calls never re-carve
+  d.B = 0; d.NB = R; d.P = 1; d.flags = flags | (p->has_kh ? KPD_FLAG_DUAL_HEAD : 0);
   if (int rc = ensure_work(p, d, kpd_plan::kOpWs, st)) return rc;
   *w = &p->work[kpd_plan::kOpWs];
   // the split-K scratch of THIS workspace: the thread's last forward may have
@@ -1539,9 +1544,12 @@ int kpd_heatmap_head(kpd_plan* p, const float* x, int R, int H, int W, int parts
   HIP_TRY(hipSetDevice(p->device));
   Work* w = nullptr;
   if (int rc = op_work(p, R, 0, st, &w)) return rc;
-  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 64, 56, 56, w->roi, w->roi_stats, st));
+  // any input sign: the split convs' bound is max |x| (hsc[r][2]), not the max
+  const bool hsplit = p->precision == KPD_PRECISION_SPLIT;
+  if (hsplit) HIP_TRY(hipMemsetAsync(w->hsc, 0, sizeof(float) * 4 * R, st));
+  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 64, 56, 56, w->roi, w->roi_stats, st, hsplit ? w->hsc + 2 : nullptr, 4));
   HIP_TRY(hipMemsetAsync(w->slot, 0, sizeof(int32_t) * R, st));   // ROI r -> heat[r] (P = 1)
-  if (int rc = run_heatmap_head(p, *w, R, 1, heat, st, parts, sp_w, nullptr, nullptr)) return rc;
+  if (int rc = run_heatmap_head(p, *w, R, 1, heat, st, parts, sp_w, nullptr, nullptr, nullptr, 1)) return rc;
   if (ch_w) HIP_TRY(hipMemcpyAsync(ch_w, w->cw, sizeof(float) * R * 64, hipMemcpyDeviceToDevice, st));
   return KPD_OK;
 }

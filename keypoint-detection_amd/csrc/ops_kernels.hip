@@ -65,7 +65,8 @@ __global__ __launch_bounds__(DT) void decode_planes_kernel(const float* __restri
   } else if constexpr (MODE == KPD_DECODE_SUBPIXEL) {
     // mass-weighted mean of the window around the maximum (row-major sums)
     if (tid == 0) {
-      const int pad = (int)param / 2, xc = mi % W, yc = mi / W;
+      // pad = window_size // 2 (Python floor: a negative window is empty -> zeros, as the reference)
+      const int pad = (int)floorf(param * 0.5f), xc = mi % W, yc = mi / W;
       const int x0 = max(0, xc - pad), x1 = min(W, xc + pad + 1), y0 = max(0, yc - pad), y1 = min(H, yc + pad + 1);
       float tot = 0.f, sx = 0.f, sy = 0.f, wm = -INFINITY;
       for (int y = y0; y < y1; ++y)
@@ -126,7 +127,8 @@ __global__ __launch_bounds__(DT) void decode_planes_kernel(const float* __restri
       if (MODE == KPD_DECODE_MODEL && vis) {
         // keypoint_model.py:268-280: conf = sigmoid(max), classes < 0.3 / < 0.7 / else
         const float conf = kpd_sigmoid(mx);
-        const int cls = conf < 0.3f ? 0 : (conf < 0.7f ? 1 : 2);
+        // compared as the reference does: conf.item() (a double) against 0.3 / 0.7
+        const int cls = (double)conf < 0.3 ? 0 : ((double)conf < 0.7 ? 1 : 2);
         vis[plane * 3 + 0] = cls == 0 ? 1.f : 0.f;
         vis[plane * 3 + 1] = cls == 1 ? 1.f : 0.f;
         vis[plane * 3 + 2] = cls == 2 ? 1.f : 0.f;
@@ -178,9 +180,13 @@ __global__ __launch_bounds__(256) void roi_align_nchw_kernel(const float* __rest
 
 // [N][C][H][W] -> [N][H][W][C], one image row per workgroup (W <= 64,
 // C <= 128) through LDS; optional per-row channel sum / max in the layout
-// roi_align_kernel writes for the HeatmapHead attention: stats [N][H][2][C].
+// roi_align_kernel writes for the HeatmapHead attention: stats [N][H][2][C];
+// optional amax[n * amax_stride] = max |x| of image n (float bits, atomicMax:
+// the caller zeroes it) -- the split heatmap convs' operand bound when the
+// input may be negative (the stand-alone HeatmapHead).
 __global__ __launch_bounds__(256) void nchw_rows_to_nhwc_kernel(const float* __restrict__ in, int C, int H, int W,
-                                                                float* __restrict__ out, float* __restrict__ stats) {
+                                                                float* __restrict__ out, float* __restrict__ stats,
+                                                                float* __restrict__ amax, int amax_stride) {
   __shared__ float t[128][65];
   const int y = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   for (int e = tid; e < C * W; e += 256) {
@@ -201,6 +207,16 @@ __global__ __launch_bounds__(256) void nchw_rows_to_nhwc_kernel(const float* __r
     float* st = stats + ((size_t)n * H + y) * 2 * C;
     st[tid] = s;
     st[C + tid] = m;
+  }
+  if (amax) {
+    float a = 0.f;
+    for (int e = tid; e < C * W; e += 256) {
+      const int c = e / W, x = e - c * W;
+      a = fmaxf(a, fabsf(t[c][x]));
+    }
+    a = wave_max(a);
+    if ((tid & 63) == 0)
+      atomicMax(reinterpret_cast<unsigned*>(amax + (size_t)n * amax_stride), __float_as_uint(a));
   }
 }
 
@@ -292,7 +308,7 @@ hipError_t launch_decode_planes(const float* heat, int planes, int H, int W, int
   switch (mode) {
     case KPD_DECODE_ARGMAX: DEC(KPD_DECODE_ARGMAX); break;
     case KPD_DECODE_SUBPIXEL:
-      if (param < 1.f) return hipErrorInvalidValue;
+      if (!(fabsf(param) < 1e9f)) return hipErrorInvalidValue;   // any finite window size (0: 1x1)
       DEC(KPD_DECODE_SUBPIXEL);
       break;
     case KPD_DECODE_SOFTARGMAX:
@@ -316,10 +332,11 @@ hipError_t launch_roi_align_nchw(const float* feat, int C, int H, int W, const f
 }
 
 hipError_t launch_nchw_rows_to_nhwc(const float* in, int N, int C, int H, int W, float* out, float* stats,
-                                    hipStream_t st) {
+                                    hipStream_t st, float* amax, int amax_stride) {
   if (N <= 0) return hipSuccess;
   if (C > 128 || W > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(nchw_rows_to_nhwc_kernel, dim3(H, N), dim3(256), 0, st, in, C, H, W, out, stats);
+  hipLaunchKernelGGL(nchw_rows_to_nhwc_kernel, dim3(H, N), dim3(256), 0, st, in, C, H, W, out, stats, amax,
+                     amax_stride);
   return hipGetLastError();
 }
 

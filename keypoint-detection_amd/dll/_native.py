@@ -357,8 +357,9 @@ def adaptive_heatmap_loss(pred: torch.Tensor, gt: torch.Tensor, target_weight: O
     loss = torch.empty((), dtype=torch.float32, device=pred.device)
     thr = torch.empty((), dtype=torch.float32, device=pred.device)
     grad = torch.empty_like(p) if want_grad else None
-    check(load().kpd_adaptive_heatmap_loss(_ptr(p), _ptr(g), _ptr(tw), B, K, H, W, float(keypoint_weight),
-                                           float(background_weight), int(bool(adaptive)), float(focal_alpha),
-                                           _ptr(loss), _ptr(grad), _ptr(thr), _stream(pred.device)),
-          "kpd_adaptive_heatmap_loss")
+    with torch.cuda.device(pred.device):
+        check(load().kpd_adaptive_heatmap_loss(_ptr(p), _ptr(g), _ptr(tw), B, K, H, W, float(keypoint_weight),
+                                               float(background_weight), int(bool(adaptive)), float(focal_alpha),
+                                               _ptr(loss), _ptr(grad), _ptr(thr), _stream(pred.device)),
+              "kpd_adaptive_heatmap_loss")
     return loss, grad, thr

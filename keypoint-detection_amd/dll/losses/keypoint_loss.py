@@ -19,12 +19,15 @@ from .. import _native
 class _AdaptiveHeatmapLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pred, gt, target_weight, kw, bw, adaptive, alpha):
+        if gt.requires_grad:
+            raise NotImplementedError("AdaptiveHeatmapLoss: the gradient with respect to gt_heatmaps is not "
+                                      "implemented (only d loss / d pred_heatmaps)")
         loss, grad, thr = _native.adaptive_heatmap_loss(pred, gt, target_weight, kw, bw, adaptive, alpha,
                                                         want_grad=pred.requires_grad)
         ctx.save_for_backward(grad if grad is not None else torch.empty(0, device=pred.device))
         ctx.pred_dtype = pred.dtype
         ctx.threshold = thr
-        return loss
+        return loss.to(pred.dtype)     # the reference's loss has pred's dtype
 
     @staticmethod
     def backward(ctx, g):

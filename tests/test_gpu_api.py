@@ -66,6 +66,13 @@ def test_decoders_vs_golden(dec):
     assert np.array_equal(decode_heatmaps(hr)[0].cpu().numpy(), g["hr_argmax_kpts"])
     np.testing.assert_allclose(decode_heatmaps_subpixel(hr)[0].cpu().numpy(), g["hr_sub_kpts"], atol=1e-6)
     np.testing.assert_allclose(decode_heatmaps_soft_argmax(hr)[0].cpu().numpy(), g["hr_sa_kpts"], atol=1e-6)
+    # window_size 0 (reference :327 pad = 0 // 2): the 1x1 window at the maximum
+    # = the argmax where the maximum is positive, zeros where its mass is 0
+    k0, s0 = decode_heatmaps_subpixel(h, window_size=0)
+    ka, sa = decode_heatmaps(h)
+    pos = (sa > 0).unsqueeze(-1)
+    torch.testing.assert_close(k0, torch.where(pos, ka, torch.zeros_like(ka)), atol=1e-6, rtol=0)
+    assert torch.equal(s0, torch.where(sa > 0, sa, torch.zeros_like(sa)))
 
 
 def test_model_helpers_vs_golden(dec, model_sd):
@@ -131,6 +138,50 @@ def test_heatmap_head_forward_vs_golden(golden_dir, model_sd, precision):
     xb = torch.rand(3, 64, 56, 56, generator=torch.Generator().manual_seed(4))
     hb, _ = m.heatmap_head(xb.to(DEV))
     np.testing.assert_allclose(hb.cpu().numpy(), O.heatmap_head(xb, model_sd).numpy(), atol=5e-5)
+
+
+def test_visibility_threshold_exact_float(model_sd):
+    """keypoint_model.py:268-280 compares conf.item() (a Python double) with
+    0.3 / 0.7: a confidence of exactly float32(0.7) = 0.69999998... is class 1
+    (occluded), float32(0.3) = 0.30000001... is class 1 too.  Maxima chosen so
+    torch's sigmoid lands on those floats exactly."""
+    m = _model(model_sd)
+    planes, want = [], []
+    for target in (0.7, 0.3):
+        t32 = torch.tensor(target, dtype=torch.float32)
+        bits0 = int(torch.logit(t32.double()).float().view(torch.int32))
+        found = None
+        for d in sorted(range(-64, 65), key=abs):     # the float32 values a few ulps around the logit
+            x = torch.tensor(bits0 + d, dtype=torch.int32).view(torch.float32)
+            if torch.sigmoid(x) == t32:
+                found = x
+                break
+        assert found is not None
+        hp = torch.full((56, 56), -3.0)
+        hp[20, 30] = found
+        planes.append(hp)
+        c = float(torch.sigmoid(found))        # the reference's conf.item()
+        want.append(0 if c < 0.3 else (1 if c < 0.7 else 2))
+    h = torch.stack(planes).view(1, 2, 56, 56).to(DEV)
+    _, v = m.decode_heatmap(h)
+    got = v.view(2, 3).argmax(dim=-1).tolist()
+    assert got == want == [1, 1]
+
+
+def test_heatmap_head_split_signed_inputs(model_sd):
+    """Stand-alone HeatmapHead in split precision on inputs of either sign: the
+    hi/lo operand scale must come from max |x| (the model's ROI features are
+    post-ReLU, a caller's need not be).  ROI 0 randn, ROI 1 all negative,
+    ROI 2 with a negative tail 50x its positive maximum."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(3, 64, 56, 56, generator=g)
+    x[1] = -x[1].abs() - 0.1
+    x[2] = torch.rand(64, 56, 56, generator=g) * 0.1
+    x[2, 5, 10:20, 10:20] = -5.0
+    m = _model(model_sd, "split")
+    h, _ = m.heatmap_head(x.to(DEV))
+    assert torch.isfinite(h).all()
+    np.testing.assert_allclose(h.cpu().numpy(), O.heatmap_head(x, model_sd).numpy(), atol=5e-5)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "split"])
