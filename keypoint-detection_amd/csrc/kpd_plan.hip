@@ -89,6 +89,7 @@ struct DevConv {
   void* ws = nullptr;
   int w_exp = 0;
   float bc = 0.f, bs = 0.f;
+  int ws_kc = 0;   // 1x1 split copy (cbody_kernel): f16 [cout_p][ws_kc][hi32 | lo32], K zero-padded to 32
 };
 struct DevDW { int C = 0, Cp = 0, k = 3, s = 1, act = 0; float* w = nullptr; float* b = nullptr; };
 struct DevSE { int C = 0, Cp = 0, sq = 0; float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr; };
@@ -125,6 +126,8 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
   float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
   float* pool = nullptr;    // [B][1024] SE channel means from the fused expand+depthwise kernel
+  float* cbd = nullptr;     // [B][cbd_floats] depthwise-output scratch of cbody_kernel (coarse body)
+  long cbd_floats = 0;
   float* separt = nullptr;  // [B][kSePartFloats] SE fc1 partials (exdw_kernel -> seproj_kernel)
   float* sc = nullptr;    // split FPN scale inputs: per-image max|tap0| [B], max|lateral1| [B] (amax_publish_img)
   // person-detector glue
@@ -397,6 +400,37 @@ int pack_split_hm(kpd_plan* p, DevConv& dc) {
   return KPD_OK;
 }
 
+// Split (fp32-accurate) copy of a 1x1 conv for cbody_kernel: the packed fp32
+// weights [cout_p][cin_p] scaled by 2^w_exp (max|w| < 2^15), each value as f16
+// hi + lo, stored per 32 input channels as [hi32 | lo32] (K zero-padded to 32).
+int pack_split_1x1(kpd_plan* p, DevConv& dc) {
+  if (dc.k != 1 || dc.bf16) return fail(KPD_EINVAL, "split 1x1 copy of a non-1x1 conv");
+  const int cin = dc.cin_p, kc = (cin + 31) / 32;
+  const size_t n = (size_t)dc.cout_p * cin;
+  std::vector<float> w(n);
+  HIP_TRY(hipMemcpy(w.data(), dc.w, n * sizeof(float), hipMemcpyDeviceToHost));
+  float mx = 0.f;
+  for (float v : w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) std::frexp(mx, &e);
+  const int w_exp = std::min(std::max(14 - e, -100), 100);
+  std::vector<_Float16> hl((size_t)dc.cout_p * kc * 64, (_Float16)0.f);
+  for (int co = 0; co < dc.cout_p; ++co)
+    for (int ci = 0; ci < cin; ++ci) {
+      const float x = std::ldexp(w[(size_t)co * cin + ci], w_exp);
+      const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+      const size_t o = ((size_t)co * kc + ci / 32) * 64 + ci % 32;
+      hl[o] = hi;
+      hl[o + 32] = lo;
+    }
+  _Float16* d = nullptr;
+  if (int rc = upload(p, hl, &d)) return rc;
+  dc.ws = d;
+  dc.w_exp = w_exp;
+  dc.ws_kc = kc;
+  return KPD_OK;
+}
+
 // FPN level 0 by linearity (fpn0x_kernel): W0 = W3 . L0 (the 3x3 conv on the
 // 16-channel stem tap through the bias-free lateral 0) and, per output position
 // class (y % 4, x % 4), the 3x3 taps summed by the lateral-1 pixel they read
@@ -499,6 +533,7 @@ int pack_fpn0x(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
 constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
 constexpr int kFuseMaxPix = 32 * 24;        // input maps up to this size take the fused expand+depthwise
 constexpr int kSePartFloats = 8192;         // per image: (Ep / CS) slices x sq fc1 partials
+constexpr int kCbFirst = 4;                 // cbody_kernel runs features.(kCbFirst + 1) .. 12
 
 struct Carver {
   char* base;
@@ -540,6 +575,11 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.sc = c.take<float>((size_t)2 * B * kAmaxStride);
   w.splitk = c.take<float>(kSplitKFloats);
   w.pool = c.take<float>((size_t)B * 1024);
+  w.cbd_floats = 0;
+  if (p->precision != KPD_PRECISION_FP32)
+    for (int i = kCbFirst; i < 11; ++i)
+      w.cbd_floats = std::max(w.cbd_floats, (long)d.h[i + 1] * d.w[i + 1] * ((pad16(p->bn[i].cfg.exp) + 31) / 32 * 32));
+  w.cbd = c.take<float>((size_t)B * w.cbd_floats);
   w.separt = c.take<float>((size_t)B * kSePartFloats);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
@@ -839,6 +879,13 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     chk(pack_conv(p, pj + ".0.weight", "", pj + ".1", 1e-3, 1, false, bn.project, missing));
   }
   chk(pack_conv(p, F + "12.0.weight", "", F + "12.1", 1e-3, 1, false, p->last, missing));
+  if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty()) {   // cbody_kernel operands
+    for (int i = kCbFirst; i < 11; ++i) {
+      if (p->bn[i].has_exp) chk(pack_split_1x1(p, p->bn[i].expand));
+      chk(pack_split_1x1(p, p->bn[i].project));
+    }
+    chk(pack_split_1x1(p, p->last));
+  }
   }
   if (p->has_fpn) {
   for (int i = 0; i < 4; ++i)
@@ -1003,6 +1050,43 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   return KPD_OK;
 }
 
+// cbody_kernel arguments for features.(kCbFirst + 1)..12 of this pass, or
+// false when the coarse-body kernel does not apply (fp32 precision, an LDS
+// image that does not fit, KPD_NO_CBODY=1 for A/B runs).
+static bool cbody_setup(kpd_plan* p, const Dims& d, Work& w, const float* x, CbodyArgs& a) {
+  static const bool off = getenv("KPD_NO_CBODY") != nullptr;
+  if (off || p->precision == KPD_PRECISION_FP32 || !p->last.ws || !w.cbd) return false;
+  a = CbodyArgs{};
+  a.x = x;
+  a.nl = 11 - kCbFirst;
+  if (a.nl > kCbMaxLayers) return false;
+  for (int l = 0; l < a.nl; ++l) {
+    const int i = kCbFirst + l;
+    const DevBneck& bn = p->bn[i];
+    if (!bn.has_exp || !bn.cfg.se || !bn.expand.ws || !bn.project.ws) return false;
+    CbLayer& L = a.L[l];
+    L.Hi = d.h[i]; L.Wi = d.w[i]; L.Ho = d.h[i + 1]; L.Wo = d.w[i + 1];
+    L.k = bn.cfg.k; L.s = bn.cfg.s;
+    L.cin_p = pad16(bn.cfg.cin); L.kc_in = bn.expand.ws_kc;
+    L.Ep = bn.dw.Cp; L.EpK = (L.Ep + 31) / 32 * 32; L.C = bn.cfg.exp;
+    if (bn.project.ws_kc * 32 != L.EpK) return false;
+    L.cout_p = bn.project.cout_p; L.act = bn.cfg.act;
+    L.res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
+    L.se = 1; L.sq = bn.se.sq;
+    L.we = static_cast<const _Float16*>(bn.expand.ws); L.we_exp = bn.expand.w_exp; L.be = bn.expand.b;
+    L.wd = bn.dw.w; L.bd = bn.dw.b;
+    L.w1 = bn.se.w1; L.b1 = bn.se.b1; L.w2t = bn.se.w2; L.b2 = bn.se.b2;
+    L.wp = static_cast<const _Float16*>(bn.project.ws); L.wp_exp = bn.project.w_exp; L.bp = bn.project.b;
+    L.tap = i + 1 == 8 ? w.o[i] : nullptr;   // features.8 output: FPN tap 2
+  }
+  a.wl = static_cast<const _Float16*>(p->last.ws); a.wl_exp = p->last.w_exp; a.bl = p->last.b;
+  a.last_cin_p = p->last.cin_p; a.last_kc = p->last.ws_kc; a.last_cout = p->last.cout_p;
+  a.tap3 = w.last;
+  a.dscr = w.cbd;
+  a.dscr_floats = w.cbd_floats;
+  return cbody_lds_bytes(a) <= 160 * 1024;
+}
+
 // HeatmapHead (heatmap_head.py:81-151) on the [R][56][56][64] NHWC ROI
 // features in w.roi with their per-row statistics in w.roi_stats: channel
 // attention, spatial attention, the three 3x3 convs and the final 1x1 +
@@ -1151,9 +1235,19 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], lin ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
+  bool cb_done = false;
   for (int i = 0; i < 11; ++i) {
     const DevBneck& bn = p->bn[i];
     const int hi = d.h[i], wi = d.w[i], ho = d.h[i + 1], wo = d.w[i + 1];
+    // features.(kCbFirst + 1)..12 as one launch, a workgroup per image (cbody.hip)
+    CbodyArgs cba;
+    if (i == kCbFirst && cbody_setup(p, d, w, x, cba)) {
+      cba.stamps = take_stamps("stamps_cbody", (size_t)B * 8);
+      HIP_TRY(launch_cbody(cba, B, st));
+      taps[2] = w.o[7];
+      cb_done = true;
+      break;
+    }
     const int inp = pad16(bn.cfg.cin);
     // coarse maps: expand + depthwise (+ SE means) fused when the image fits LDS
     ExDwArgs xa{};
@@ -1270,9 +1364,10 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     if (i + 1 == 3) taps[1] = x;
     if (i + 1 == 8) taps[2] = x;
   }
-  if (int rc = conv(p->last, x, B, d.h[11], d.w[11], pad16(96), w.last, ACT_HSWISH, nullptr, 0, 0, nullptr,
-                    nullptr, 0, 0, st))
-    return rc;
+  if (!cb_done)
+    if (int rc = conv(p->last, x, B, d.h[11], d.w[11], pad16(96), w.last, ACT_HSWISH, nullptr, 0, 0, nullptr,
+                      nullptr, 0, 0, st))
+      return rc;
   taps[3] = w.last;
   body_stage.reset();
 
