@@ -68,7 +68,7 @@ __host__ __device__ inline CbLds cb_layout(const CbodyArgs& a) {
 }
 
 __device__ __forceinline__ void cstamp(unsigned long long* st, int i) {
-  if (st && threadIdx.x == 0) st[(size_t)blockIdx.x * 64 + (i & 63)] = __builtin_amdgcn_s_memrealtime();
+  if (st && threadIdx.x == 0) st[(size_t)blockIdx.x * 128 + (i & 127)] = __builtin_amdgcn_s_memrealtime();
 }
 
 __device__ __forceinline__ void split8(const float* v, float sc, f16x8& hi, f16x8& lo) {
@@ -118,6 +118,12 @@ __device__ int build_xs(const float* X, char* XS, int P, int cin_p, int kc, cons
   return ex;
 }
 
+// workgroup barrier that orders LDS only: the wave's global stores and
+// prefetch loads stay in flight across it (they are waited for where used)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ void lds_max(unsigned* slot, float v) {
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(slot, __float_as_uint(v));
@@ -130,7 +136,7 @@ __device__ __forceinline__ void lds_max(unsigned* slot, float v) {
 // fixed butterfly, per wave into RED [NW][RW]; max|d| into *dmax.
 template <int K, int S, int XT>
 __device__ void depthwise_round(const CbLayer& L, const float* E, const float* WD, float* D, float* RED,
-                                unsigned* dmax, int c0, int rc) {
+                                unsigned* dmax, int c0, int rc, int dbg) {
   constexpr int PD = (K - 1) / 2, NC = (XT - 1) * S + K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = tid & 15;
   const int nxt = (L.Wo + XT - 1) / XT, nsp = L.Ho * nxt;
@@ -173,7 +179,7 @@ __device__ void depthwise_round(const CbLayer& L, const float* E, const float* W
       v.x = kpd_act(a[o].x + b.x, ACT_HSWISH); v.y = kpd_act(a[o].y + b.y, ACT_HSWISH);
       v.z = kpd_act(a[o].z + b.z, ACT_HSWISH); v.w = kpd_act(a[o].w + b.w, ACT_HSWISH);
       const int op = oy * L.Wo + ox0 + o;
-      *reinterpret_cast<float4*>(D + (size_t)op * L.EpK + c0 + q * 4) = v;
+      if (!(dbg & 1)) *reinterpret_cast<float4*>(D + (size_t)op * L.EpK + c0 + q * 4) = v;
       psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
       m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
@@ -235,7 +241,8 @@ __device__ __forceinline__ void store_wd(const CbLayer& L, float* WD, int rc, fl
 // weights, bias and depthwise weights are loaded into registers while round
 // r's depthwise runs.
 template <int KC>
-__device__ void block_rounds(const CbLayer& L, const Smem& s, float* D, int ex, unsigned long long* stamps, int& st) {
+__device__ void block_rounds(const CbLayer& L, const Smem& s, float* D, int ex, unsigned long long* stamps, int& st,
+                             int& st2, int dbg) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
   const int Pin = L.Hi * L.Wi, Po = L.Ho * L.Wo, mtin = (Pin + 15) / 16, nt = wave & 3;
   const float eunsc = ldexpf(1.f, -(ex + L.we_exp));
@@ -271,17 +278,21 @@ __device__ void block_rounds(const CbLayer& L, const Smem& s, float* D, int ex, 
         }
       }
     }
-    __syncthreads();
+    if (dbg & 2) lds_barrier();
+    else __syncthreads();
+    if (st2 < 64) cstamp(stamps, 64 + st2);
+    ++st2;
     if (r + 1 < nr) {   // next round's operands in flight during this depthwise
       const int rcn = min(RW, L.Ep - c0 - RW);
       load_bfrag<KC>(L, c0 + RW, rcn, bnext);
       wdr = load_wd(L, c0 + RW, rcn);
     }
-    if (L.k == 5 && L.s == 1) depthwise_round<5, 1, 4>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc);
-    else if (L.k == 5 && L.s == 2) depthwise_round<5, 2, 2>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc);
-    else if (L.k == 3 && L.s == 1) depthwise_round<3, 1, 4>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc);
-    else depthwise_round<3, 2, 2>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc);
-    __syncthreads();
+    if (L.s == 1) depthwise_round<5, 1, 4>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc, dbg);
+    else depthwise_round<5, 2, 2>(L, s.E, s.WD, D, s.RED, &s.MISC[1], c0, rc, dbg);
+    if (dbg & 2) lds_barrier();
+    else __syncthreads();
+    if (st2 < 64) cstamp(stamps, 64 + st2);
+    ++st2;
     bcur = bnext;
     rc_prev = rc;
   }
@@ -345,57 +356,74 @@ __device__ void squeeze_excite(const CbLayer& L, const Smem& s) {
 // unit = (M tile, NG N tiles); the K loop is software-pipelined two chunks
 // deep (each chunk: 8 d values of the lane's row + NG B fragments)
 template <int NG>
+__device__ __forceinline__ void proj_load(const float* drow, const char* wbase, int kc, int kcp, float4& d0, float4& d1,
+                                          f16x8 (&bh)[NG], f16x8 (&bl)[NG]) {
+  // always in bounds (rows are EpK wide); channels >= Ep are zeroed in proj_compute
+  d0 = *reinterpret_cast<const float4*>(drow + kc * 32);
+  d1 = *reinterpret_cast<const float4*>(drow + kc * 32 + 4);
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const char* wr = wbase + ((size_t)j * 16 * kcp + kc) * 128;
+    bh[j] = *reinterpret_cast<const f16x8*>(wr);
+    bl[j] = *reinterpret_cast<const f16x8*>(wr + 64);
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void proj_compute(const float* SC, int kc, int g, float dsc, bool live, float4 d0, float4 d1,
+                                             const f16x8 (&bh)[NG], const f16x8 (&bl)[NG], f32x4 (&acc)[NG]) {
+  const float4 s0 = *reinterpret_cast<const float4*>(SC + (live ? kc * 32 + g * 8 : 0));
+  const float4 s1 = *reinterpret_cast<const float4*>(SC + (live ? kc * 32 + g * 8 + 4 : 0));
+  if (!live) {   // padding channels of D hold no data: SC is 0 there, but 0 * garbage may be NaN
+    d0 = make_float4(0.f, 0.f, 0.f, 0.f);
+    d1 = d0;
+  }
+  f16x8 ah, al;
+  {
+    const float v0 = d0.x * s0.x * dsc, v1 = d0.y * s0.y * dsc, v2 = d0.z * s0.z * dsc, v3 = d0.w * s0.w * dsc;
+    const float v4 = d1.x * s1.x * dsc, v5 = d1.y * s1.y * dsc, v6 = d1.z * s1.z * dsc, v7 = d1.w * s1.w * dsc;
+    ah[0] = (_Float16)v0; ah[1] = (_Float16)v1; ah[2] = (_Float16)v2; ah[3] = (_Float16)v3;
+    ah[4] = (_Float16)v4; ah[5] = (_Float16)v5; ah[6] = (_Float16)v6; ah[7] = (_Float16)v7;
+    al[0] = (_Float16)(v0 - (float)ah[0]); al[1] = (_Float16)(v1 - (float)ah[1]);
+    al[2] = (_Float16)(v2 - (float)ah[2]); al[3] = (_Float16)(v3 - (float)ah[3]);
+    al[4] = (_Float16)(v4 - (float)ah[4]); al[5] = (_Float16)(v5 - (float)ah[5]);
+    al[6] = (_Float16)(v6 - (float)ah[6]); al[7] = (_Float16)(v7 - (float)ah[7]);
+  }
+#pragma unroll
+  for (int j = 0; j < NG; ++j) acc[j] = mma3(ah, al, bh[j], bl[j], acc[j]);
+}
+
+// project 1x1: X[px][o] = (D * s)[px][:] . Wp[o][:] 2^-(ed + wp_exp) + bp (+ X)
+// unit = (M tile, NG N tiles); the K loop is software-pipelined two chunks
+// deep (each chunk: 8 d values of the lane's row + NG B fragments)
+template <int NG>
 __device__ void project(const CbLayer& L, const Smem& s, const float* D) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
   const int Po = L.Ho * L.Wo, mto = (Po + 15) / 16, ntiles = L.cout_p / 16, kcp = L.EpK / 32;
   const int units = mto * (ntiles / NG);
   const int ed = split_exp_of(__uint_as_float(s.MISC[1]));
   const float dsc = ldexpf(1.f, ed), punsc = ldexpf(1.f, -(ed + L.wp_exp));
-  struct Stage { float4 d0, d1; f16x8 bh[NG], bl[NG]; };
   float m = 0.f;
   for (int u = wave; u < units; u += NW) {
     const int mt = u % mto, nt0 = (u / mto) * NG;
     const int pxa = min(mt * 16 + r16, Po - 1);
     const float* drow = D + (size_t)pxa * L.EpK + g * 8;
     const char* wbase = reinterpret_cast<const char*>(L.wp) + ((size_t)(nt0 * 16 + r16) * kcp) * 128 + g * 16;
-    auto load = [&](int kc, Stage& S) {
-      if (kc * 32 + g * 8 < L.Ep) {
-        S.d0 = *reinterpret_cast<const float4*>(drow + kc * 32);
-        S.d1 = *reinterpret_cast<const float4*>(drow + kc * 32 + 4);
-      } else {
-        S.d0 = make_float4(0.f, 0.f, 0.f, 0.f);
-        S.d1 = S.d0;
-      }
-#pragma unroll
-      for (int j = 0; j < NG; ++j) {
-        const char* wr = wbase + ((size_t)j * 16 * kcp + kc) * 128;
-        S.bh[j] = *reinterpret_cast<const f16x8*>(wr);
-        S.bl[j] = *reinterpret_cast<const f16x8*>(wr + 64);
-      }
-    };
     f32x4 acc[NG];
 #pragma unroll
     for (int j = 0; j < NG; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto compute = [&](int kc, const Stage& S) {
-      const float4 s0 = *reinterpret_cast<const float4*>(s.SC + kc * 32 + g * 8);
-      const float4 s1 = *reinterpret_cast<const float4*>(s.SC + kc * 32 + g * 8 + 4);
-      const float v[8] = {S.d0.x * s0.x, S.d0.y * s0.y, S.d0.z * s0.z, S.d0.w * s0.w,
-                          S.d1.x * s1.x, S.d1.y * s1.y, S.d1.z * s1.z, S.d1.w * s1.w};
-      f16x8 ah, al;
-      split8(v, dsc, ah, al);
-#pragma unroll
-      for (int j = 0; j < NG; ++j) acc[j] = mma3(ah, al, S.bh[j], S.bl[j], acc[j]);
-    };
-    Stage s0, s1;
-    load(0, s0);
-    if (kcp > 1) load(1, s1);
+    float4 da0, da1, db0, db1;
+    f16x8 bha[NG], bla[NG], bhb[NG], blb[NG];
+    // straight-line double-buffered loop: every load unconditional (the chunk
+    // index clamped; an out-of-range chunk computes with live = false, i.e. a
+    // zero A), so the compiler's vmcnt waits stay exact across iterations
+    proj_load<NG>(drow, wbase, 0, kcp, da0, da1, bha, bla);
+    proj_load<NG>(drow, wbase, min(1, kcp - 1), kcp, db0, db1, bhb, blb);
     for (int kc = 0; kc < kcp; kc += 2) {
-      compute(kc, s0);
-      if (kc + 2 < kcp) load(kc + 2, s0);
-      if (kc + 1 < kcp) {
-        compute(kc + 1, s1);
-        if (kc + 3 < kcp) load(kc + 3, s1);
-      }
+      proj_compute<NG>(s.SC, kc, g, dsc, kc * 32 + g * 8 < L.Ep, da0, da1, bha, bla, acc);
+      proj_load<NG>(drow, wbase, min(kc + 2, kcp - 1), kcp, da0, da1, bha, bla);
+      proj_compute<NG>(s.SC, kc + 1, g, dsc, kc + 1 < kcp && (kc + 1) * 32 + g * 8 < L.Ep, db0, db1, bhb, blb, acc);
+      proj_load<NG>(drow, wbase, min(kc + 3, kcp - 1), kcp, db0, db1, bhb, blb);
     }
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
@@ -432,7 +460,7 @@ __global__ __launch_bounds__(NT) void cbody_kernel(const CbodyArgs a) {
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   float* D = a.dscr + (size_t)n * a.dscr_floats;
-  int st = 0;
+  int st = 0, st2 = 0;   // stamp slots: phases 0.., rounds 64..
   cstamp(a.stamps, st++);
   if (tid < 16) s.MISC[tid] = 0u;
   __syncthreads();
@@ -455,8 +483,8 @@ __global__ __launch_bounds__(NT) void cbody_kernel(const CbodyArgs a) {
     __syncthreads();
     if (tid == 0) { s.MISC[0] = 0u; s.MISC[1] = 0u; }
     cstamp(a.stamps, st++);
-    if (L.kc_in == 2) block_rounds<2>(L, s, D, ex, a.stamps, st);
-    else block_rounds<3>(L, s, D, ex, a.stamps, st);
+    if (L.kc_in == 2) block_rounds<2>(L, s, D, ex, a.stamps, st, st2, a.dbg);
+    else block_rounds<3>(L, s, D, ex, a.stamps, st, st2, a.dbg);
     squeeze_excite(L, s);
     cstamp(a.stamps, st++);
     const int mto = (Po + 15) / 16;
@@ -498,7 +526,7 @@ __global__ __launch_bounds__(NT) void cbody_kernel(const CbodyArgs a) {
       }
     };
     LStage S;
-    if (wave < units) load(wave, S);
+    load(min(wave, units - 1), S);
     for (int u = wave; u < units; u += NW) {
       const int mt = u % mt_n, c0 = (u / mt_n) * 64;
       const int pxa = min(mt * 16 + r16, P - 1);
@@ -515,7 +543,7 @@ __global__ __launch_bounds__(NT) void cbody_kernel(const CbodyArgs a) {
       float bb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bb[j] = S.b[j];
-      if (u + NW < units) load(u + NW, S);
+      load(min(u + NW, units - 1), S);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int oc = c0 + j * 16 + r16;
@@ -544,7 +572,7 @@ hipError_t launch_cbody(const CbodyArgs& a, int N, hipStream_t st) {
     const CbLayer& L = a.L[l];
     const bool ok = L.act == ACT_HSWISH && (L.kc_in == 2 || L.kc_in == 3) && L.cin_p % 16 == 0 && L.kc_in * 32 >= L.cin_p && L.Ep % 16 == 0 && L.EpK % 32 == 0 &&
                     L.EpK >= L.Ep && L.Ep <= kMaxEp && L.EpK <= kMaxEp && L.C <= L.Ep && L.cout_p % 16 == 0 &&
-                    L.cout_p <= 96 && (L.k == 3 || L.k == 5) && (L.s == 1 || L.s == 2) && L.sq <= kMaxSq &&
+                    L.cout_p <= 96 && L.k == 5 && (L.s == 1 || L.s == 2) && L.sq <= kMaxSq &&
                     L.we && L.be && L.wd && L.bd && L.wp && L.bp && (!L.se || (L.w1 && L.b1 && L.w2t && L.b2)) &&
                     (!L.res || (L.cin_p == L.cout_p && L.Hi == L.Ho && L.Wi == L.Wo)) &&
                     (l == 0 || (a.L[l - 1].Ho == L.Hi && a.L[l - 1].Wo == L.Wi && a.L[l - 1].cout_p == L.cin_p));

@@ -198,7 +198,8 @@ struct CbodyArgs {
   float* tap3;                 // [N][P][576]
   float* dscr;                 // per-image depthwise-output scratch
   long dscr_floats;            // floats per image
-  unsigned long long* stamps;  // diagnostic phase stamps [N][64] (KPD_STAMPS), normally null
+  unsigned long long* stamps;  // diagnostic phase stamps [N][128] (KPD_STAMPS), normally null
+  int dbg;                     // ablations (KPD_CBODY_DBG): 1 = no depthwise-output stores (wrong results)
 };
 size_t cbody_lds_bytes(const CbodyArgs& a);
 hipError_t launch_cbody(const CbodyArgs& a, int N, hipStream_t st);

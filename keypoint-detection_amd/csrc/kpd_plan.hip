@@ -1054,8 +1054,12 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
 // false when the coarse-body kernel does not apply (fp32 precision, an LDS
 // image that does not fit, KPD_NO_CBODY=1 for A/B runs).
 static bool cbody_setup(kpd_plan* p, const Dims& d, Work& w, const float* x, CbodyArgs& a) {
-  static const bool off = getenv("KPD_NO_CBODY") != nullptr;
-  if (off || p->precision == KPD_PRECISION_FP32 || !p->last.ws || !w.cbd) return false;
+  // opt-in (KPD_CBODY=1): measured slower than the batched path at C2
+  // (0.56 vs 0.27 ms for features.5..12 at 64 images: one CU per image leaves
+  // 3/4 of the chip idle and the per-image chain is latency-bound) and equal
+  // at C3 (body)
+  static const bool on = getenv("KPD_CBODY") != nullptr && atoi(getenv("KPD_CBODY")) != 0;
+  if (!on || p->precision == KPD_PRECISION_FP32 || !p->last.ws || !w.cbd) return false;
   a = CbodyArgs{};
   a.x = x;
   a.nl = 11 - kCbFirst;
@@ -1242,7 +1246,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     // features.(kCbFirst + 1)..12 as one launch, a workgroup per image (cbody.hip)
     CbodyArgs cba;
     if (i == kCbFirst && cbody_setup(p, d, w, x, cba)) {
-      cba.stamps = take_stamps("stamps_cbody", (size_t)B * 8);
+      cba.stamps = take_stamps("stamps_cbody", (size_t)B * 16);
+      static const int cb_dbg = getenv("KPD_CBODY_DBG") ? atoi(getenv("KPD_CBODY_DBG")) : 0;   // ablations
+      cba.dbg = cb_dbg;
       HIP_TRY(launch_cbody(cba, B, st));
       taps[2] = w.o[7];
       cb_done = true;

@@ -74,11 +74,16 @@ def main():
     ap.add_argument("outdir")
     ap.add_argument("--precision", default="split")
     ap.add_argument("--skip", type=int, default=2)
+    ap.add_argument("--take", type=int, default=0, help="forwards kept after --skip (0 = all): the bench's timed region")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     # repo-relative source path (the GPU box's scratch root differs per call)
     src = os.path.relpath(os.path.abspath(a.outdir), os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))
-    res = {"_meta": {"source": src, "precision": a.precision, "skip_forwards": a.skip}}
+    res = {"_meta": {"source": src, "precision": a.precision, "skip_forwards": a.skip, "take_forwards": a.take}}
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import kernel_src_hash
+    res["_meta"]["src_hash"] = kernel_src_hash()
     # ---- kernel trace
     kt = []
     tdir = os.path.join(a.outdir, "trace") if os.path.isdir(os.path.join(a.outdir, "trace")) else a.outdir
@@ -89,6 +94,8 @@ def main():
                 kt.append((t0, short(r["Kernel_Name"]), (t1 - t0) * 1e-3))
     if kt:
         fw = forwards(kt, key=lambda r: r[0])[a.skip:]
+        if a.take:
+            fw = fw[:a.take]
         st, kn = defaultdict(list), defaultdict(list)
         for f in fw:
             per = defaultdict(float)   # a stage may be several launches (conv 3 + its tail launch): summed
@@ -102,7 +109,8 @@ def main():
         res["_meta"]["forward_kernel_us"] = round(sum(sum(v) for v in kn.values()) / max(len(fw), 1), 2)
         for lab, v in st.items():
             res[f"{lab}:{a.precision}"] = {"avg_us": round(sum(v) / len(v), 3), "min_us": round(min(v), 3),
-                                           "max_us": round(max(v), 3), "launches": len(v)}
+                                           "max_us": round(max(v), 3), "launches": len(v),
+                                           "src_hash": res["_meta"]["src_hash"]}
         res["kernels_us"] = {k: {"avg_us": round(sum(v) / len(v), 3), "calls": len(v),
                                  "per_forward_us": round(sum(v) / max(len(fw), 1), 3)}
                              for k, v in sorted(kn.items(), key=lambda kv: -sum(kv[1]))}
@@ -124,7 +132,8 @@ def main():
             per_tag[tag].append((did, names[(tag, did)], cs))
         agg = defaultdict(lambda: defaultdict(list))
         for tag, rows in per_tag.items():
-            for f in forwards(rows, key=lambda r: r[0])[a.skip:]:
+            fws = forwards(rows, key=lambda r: r[0])[a.skip:]
+            for f in (fws[:a.take] if a.take else fws):
                 per = defaultdict(lambda: defaultdict(float))
                 for (name, cs), lab in zip(f, label([n for n, _ in f])):
                     for c, v in cs.items():
@@ -144,6 +153,7 @@ def main():
                 e["mfma_busy_frac"] = e["SQ_VALU_MFMA_BUSY_CYCLES"] / (128.0 * e["GRBM_GUI_ACTIVE"])
             if ":" in k:
                 e["source"] = src
+                e["src_hash"] = res["_meta"]["src_hash"]
     txt = json.dumps(res, indent=1)
     if a.out:
         with open(a.out, "w") as fh:

@@ -35,16 +35,22 @@ def main():
             m(batch)
     torch.cuda.synchronize()
     buf = plan.debug_buffer("stamps_cbody")
-    st = buf.view(torch.int64).cpu().numpy().reshape(B, 64)
+    st = buf.view(torch.int64).cpu().numpy().reshape(B, 128)
+    rounds = st[:, 64:]
+    st = st[:, :64]
     used = [c for c in range(64) if (st[:, c] != 0).all()]
     t = st[:, used].astype(np.float64) * 0.01   # us
     t0 = t[:, 0].min()
     t -= t0
     ph = np.diff(t, axis=1)
-    names = ["load X"]
+    names = ["load X + xs"]
     for i in range(5, 12):
-        names += [f"f{i} xs", f"f{i} rounds", f"f{i} se", f"f{i} proj"]
-    names += ["f12"]
+        names += [f"f{i} rounds", f"f{i} se", f"f{i} proj", f"f{i} tap+xs"]
+    names[-1] = "f12"
+    ru = [c for c in range(64) if (rounds[:, c] != 0).all()]
+    rt = rounds[:, ru].astype(np.float64) * 0.01 - t0
+    print("round stamps (expand done, depthwise done), median us from kernel start:")
+    print("  " + " ".join(f"{v:.1f}" for v in np.median(rt, axis=0)))
     print(f"workgroups {B}: start p50 {np.median(t[:, 0]):.1f} max {t[:, 0].max():.1f} us; "
           f"end p50 {np.median(t[:, -1]):.1f} max {t[:, -1].max():.1f} us")
     for j in range(ph.shape[1]):
