@@ -41,7 +41,10 @@ def _worker(rank, world, store, total, q):
         images[:, 0, 0, 0] = torch.arange(total, dtype=torch.float32)
         boxes = torch.rand(total, 3, 4)
         out = sharded_forward(FakeModel(), images, boxes)
-        q.put((rank, out["keypoints"], out["visibilities"], [shard_range(total, world, r) for r in range(world)]))
+        # numpy arrays travel by value: a torch tensor would be shared through a
+        # file descriptor the exiting worker may close before the parent reads it
+        q.put((rank, out["keypoints"].numpy(), out["visibilities"].numpy(),
+               [shard_range(total, world, r) for r in range(world)]))
     finally:
         dist.destroy_process_group()
 
@@ -55,7 +58,7 @@ def test_sharded_forward_gloo(total):
     procs = [ctx.Process(target=_worker, args=(r, world, store, total, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [(r, torch.from_numpy(k), torch.from_numpy(v), rg) for r, k, v, rg in (q.get(timeout=120) for _ in range(world))]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -123,7 +126,7 @@ def _oracle_worker(rank, world, store, q):
         torch.set_num_threads(2)
         sd, images, boxes = _oracle_case()
         out = sharded_forward(OracleModel(sd), images, boxes, keys=("keypoints", "visibilities", "heatmap"))
-        q.put((rank, {k: v.clone() for k, v in out.items()}))
+        q.put((rank, {k: v.numpy().copy() for k, v in out.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -139,7 +142,7 @@ def test_sharded_forward_oracle_gloo():
     procs = [ctx.Process(target=_oracle_worker, args=(r, world, store, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
+    res = {r: {k: torch.from_numpy(v) for k, v in d.items()} for r, d in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
