@@ -357,11 +357,14 @@ def test_c4_rank_shard_bit_identical(precision):
         assert torch.equal(got, full[k]), k
     assert torch.equal(torch.stack([b for p in parts for b in p["boxes"]]), torch.stack(full["boxes"]))
     assert full["keypoints"].shape == (256, 5, 1, 17, 2)
-    # a few images against the oracle on the detected boxes
-    ref = O.forward(sd, {"image": img[:3].cpu(), "bboxes": torch.stack(full["boxes"][:3]).cpu()}, dual_head=True)
+    # images against the oracle on the detected boxes: the first three, both
+    # sides of every split boundary and the last one
+    sel = [0, 1, 2, 36, 37, 38, 159, 160, 255]
+    ref = O.forward(sd, {"image": img[sel].cpu(), "bboxes": torch.stack([full["boxes"][i] for i in sel]).cpu()},
+                    dual_head=True)
     tol = 1e-5 if precision != "mixed" else 1e-3
-    np.testing.assert_allclose(full["keypoints"][:3].cpu().numpy(), ref["keypoints"].numpy(), atol=tol)
-    np.testing.assert_allclose(full["kh_keypoints"][:3].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol)
+    np.testing.assert_allclose(full["keypoints"][sel].cpu().numpy(), ref["keypoints"].numpy(), atol=tol)
+    np.testing.assert_allclose(full["kh_keypoints"][sel].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol)
 
 
 def test_saturated_heatmaps_finite(model_sd):
@@ -380,3 +383,42 @@ def test_saturated_heatmaps_finite(model_sd):
         h = out["heatmap"]
         assert torch.isfinite(h).all() and (h >= 0).all() and (h <= 1).all(), precision
         assert torch.isfinite(out["keypoints"]).all(), precision
+
+
+@pytest.mark.parametrize("precision", ["split"])
+def test_c5_full_rank_share(precision):
+    """BASELINE C5's per-GPU share at full size: 256 images (2048 / 8) of
+    384x288, 5 given boxes per image, heatmap head + KEYPOINT_HEAD (1,280
+    ROIs).  Bit-identity of every output across two different shard splits,
+    finite heatmaps in [0, 1], and 5 images against the oracle -- among them
+    an image with padding slots (zero boxes mid-list and at the end) and the
+    dynamic-range outlier."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m, sd = _dual_model(precision)
+    m.streams = 2
+    B = 256
+    img = synthetic_images(B, 3, 384, 288, seed=61, device=DEV)
+    img[100] *= 4.0                            # larger dynamic range (scores stay untied)
+    boxes = synthetic_boxes(B, 5, seed=62, device=DEV)
+    boxes[7, 1] = 0.0                          # zero box mid-list: compacted, slot 4 padded
+    boxes[7, 3] = 0.0
+    boxes[200, 2:] = 0.0                       # trailing padding slots
+    with torch.no_grad():
+        full = m({"image": img, "bboxes": boxes})
+        parts = [m({"image": img[a:b], "bboxes": boxes[a:b]}) for a, b in ((0, 100), (100, 101), (101, 256))]
+    keys = ("keypoints", "visibilities", "heatmap", "kh_keypoints", "kh_visibilities")
+    for k in keys:
+        assert torch.equal(torch.cat([p[k] for p in parts], dim=0), full[k]), k
+    h = full["heatmap"]
+    assert h.shape == (B, 5, 17, 56, 56)
+    assert torch.isfinite(h).all() and (h >= 0).all() and (h <= 1).all()
+    assert not full["keypoints"][7, 3:].any() and not h[7, 3:].any()
+    assert not full["keypoints"][200, 2:].any()
+    sel = [0, 7, 100, 200, 255]
+    ref = O.forward(sd, {"image": img[sel].cpu(), "bboxes": boxes[sel].cpu()}, dual_head=True)
+    np.testing.assert_allclose(full["keypoints"][sel].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    np.testing.assert_allclose(h[sel].cpu().numpy(), ref["heatmap"].numpy(), atol=5e-5)
+    assert torch.equal(full["visibilities"][sel].cpu(), ref["visibilities"])
+    np.testing.assert_allclose(full["kh_keypoints"][sel].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=1e-5)
+    np.testing.assert_allclose(full["kh_visibilities"][sel].cpu().numpy(), ref["kh_visibilities"].numpy(),
+                               atol=1e-5)

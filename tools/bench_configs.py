@@ -12,10 +12,19 @@ times C2, the metric's config).  One JSON line per config:
   C5  per-GPU share of B=2048 on 8 GPUs = 256 images, 384x288, 5 given boxes
       per image, heatmap head + KEYPOINT_HEAD
 
-Synthetic seeded inputs and weights (as bench.py); HIP events around K
-forwards after W warm-ups, single process, one GPU.
+Synthetic seeded inputs and weights (as bench.py); wall clock around K
+forwards after W warm-ups (past the ~30-forward clock ramp), single process,
+one GPU.  C3 / C5 lines also carry, as bench.py's line does:
+  stages_ms   one single-stream forward with every stage's HIP events (per
+              launch; a pass of at most max_pass_images images)
+  roofline    the dominant MFMA stage: ALGORITHMIC flops per launch / its mean
+              launch time over K single-stream forwards (HIP events on the
+              launch stream), against the dense MFMA peak of the dtype issued
+  cpu_baseline  the golden-pinned oracle (dual head; C3 with the detector
+              glue) on a bounded sample of the same workload, this host's CPU
+              share
 
-    python tools/bench_configs.py [--steps 10] [--warmup 3] [--precision mixed]
+    python tools/bench_configs.py [--steps 20] [--warmup 30] [--precision mixed]
 """
 import argparse
 import json
@@ -75,10 +84,98 @@ def c1_latency(m, c, precision):
             "max_abs_dkpt_vs_cpu": float((out["keypoints"].cpu() - ref["keypoints"]).abs().max())}
 
 
+def kh_flops_per_roi(c=128, fine=64, reg=32, vis=32, h=56, w=56):
+    """KEYPOINT_HEAD algorithmic flops per ROI (keypoint_head.py:9-90): 2*MAC
+    of its convs and linears at the ROI resolution (BN folded)."""
+    hw = h * w
+    f = 2.0 * hw * (c * (c // 2) + (c // 2))                        # spatial attention 1x1 C->C/2->1
+    f += 2.0 * hw * (c * fine * 9 + (c * fine if c != fine else 0))  # ResidualBlock(C->64) (+ downsample)
+    f += 2.0 * hw * (fine * reg * 9 + (fine * reg if fine != reg else 0))
+    f += 2.0 * hw * reg * (reg // 2) * 9                               # 3x3 32->16
+    f += 2.0 * ((reg // 2) * (h // 4) * (w // 4) * 256 + 256 * 34)    # regression linears
+    f += 2.0 * hw * c * vis * 9 + 2.0 * (vis * 16 * 128 + 128 * 51)   # visibility branch
+    return f
+
+
+def config_flops(H, W, P, detect):
+    """Per-image algorithmic flops of a C3 / C5 forward: backbone
+    + FPN level 0 + P x (heatmap head + KEYPOINT_HEAD) (+ the detector's 1x1
+    heads on the 56x56-pooled 128-channel level 0)."""
+    import bench
+    fl = dict(bench.flops_per_image(H, W, P))
+    kh = kh_flops_per_roi()
+    fl["keypoint_head"] = P * kh
+    fl["total"] += P * kh + (2.0 * 3136 * 128 * 45 if detect else 0.0)
+    return fl
+
+
+def stage_breakdown(m, batch, iters=1):
+    """Single-stream per-stage means (ms per launch) and launches per forward."""
+    plan = m.native_plan(torch.device("cuda", 0))
+    keep = m.streams
+    m.streams = 1
+    st = {}
+    with torch.no_grad():
+        torch.cuda.synchronize()
+        plan.timing(True)
+        for _ in range(iters):
+            m(batch)
+        torch.cuda.synchronize()
+        plan.timing(False)
+    from dll import _native
+    for s_ in _native.STAGES:
+        ms, n = plan.timing_query(s_)
+        if n:
+            st[s_] = (ms / n, n // iters)
+    m.streams = keep
+    return st
+
+
+def dominant_timed(m, batch, stage, steps):
+    """Mean launch time of one stage over `steps` single-stream forwards (HIP
+    events on the launch stream around that stage only)."""
+    plan = m.native_plan(torch.device("cuda", 0))
+    keep = m.streams
+    m.streams = 1
+    with torch.no_grad():
+        torch.cuda.synchronize()
+        plan.timing(True, stage=stage)
+        for _ in range(steps):
+            m(batch)
+        torch.cuda.synchronize()
+        plan.timing(False)
+    m.streams = keep
+    ms, n = plan.timing_query(stage)
+    return (ms / n if n else None), n
+
+
+def cpu_sample(sd, img, boxes, detect, threads, runs=3):
+    """The oracle on a bounded sample: dual head, and for C3 the detector glue
+    (oracle person_detect on the oracle's own FPN level 0) before the heads."""
+    from oracle import kpd_oracle as O
+    torch.set_num_threads(threads)
+
+    def fwd():
+        if detect:
+            return O.forward(sd, {"image": img}, dual_head=True,
+                             detect=dict(conf_threshold=0.3, iou_threshold=0.3, max_persons=5))
+        return O.forward(sd, {"image": img, "bboxes": boxes}, dual_head=True)
+
+    out = fwd()
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fwd()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return out, img.shape[0] / ts[len(ts) // 2], ts
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--cpu-sample", type=int, default=4, help="images in the C3 / C5 CPU-baseline sample (0 = none)")
     ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"])
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--configs", default="C1,C3,C5")
@@ -110,9 +207,49 @@ def main():
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
         persons = int(out["keypoints"].shape[1])
-        print(json.dumps({"config": name, "workload": c["desc"], "precision": a.precision, "streams": a.streams,
-                          "images_per_s": round(c["B"] * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
-                          "persons_per_image": persons, "steps": a.steps, "warmup": a.warmup}), flush=True)
+        line = {"config": name, "workload": c["desc"], "precision": a.precision, "streams": a.streams,
+                "images_per_s": round(c["B"] * a.steps / el, 1), "ms_per_step": round(el / a.steps * 1e3, 3),
+                "persons_per_image": persons, "steps": a.steps, "warmup": a.warmup}
+        import bench
+        detect = not c["P"]
+        fl = config_flops(c["H"], c["W"], persons, detect)
+        line["gflop_per_image"] = round(fl["total"] / 1e9, 3)
+        line["achieved_tflops_total"] = round(fl["total"] * c["B"] * a.steps / el / 1e12, 2)
+        bd = stage_breakdown(m, batch)
+        line["stages_ms"] = {k: round(v[0], 4) for k, v in bd.items()}
+        line["stage_launches_per_forward"] = {k: v[1] for k, v in bd.items()}
+        mfma = [k for k in ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3") if k in bd]
+        dom = max(mfma, key=lambda k: bd[k][0])
+        dms, dn = dominant_timed(m, batch, dom, a.steps)
+        nl = bd[dom][1]
+        stages = {k: v[0] for k, v in bd.items()}
+        stages[dom] = dms
+        roof = bench.roofline(a.precision, stages, fl, c["B"] / nl, c["H"], c["W"], None, dom)
+        roof["launches_timed"] = dn
+        roof["images_per_launch"] = c["B"] / nl
+        roof["timing"] = "HIP events around every launch of this stage in single-stream forwards after the warm-up"
+        line["roofline"] = roof
+        kh = bd.get("keypoint_head")
+        if kh:
+            line["keypoint_head_tflops"] = round(fl["keypoint_head"] * c["B"] / nl / (kh[0] * 1e-3) / 1e12, 2)
+        if a.cpu_sample > 0:
+            ci = bench.host_cpu_info()
+            S = min(a.cpu_sample, c["B"])
+            sd = {k: v.cpu() for k, v in m.state_dict().items()}
+            ref, rate, ts = cpu_sample(sd, img[:S].cpu(), batch["bboxes"][:S].cpu() if c["P"] else None, detect,
+                                       ci["threads"])
+            line["cpu_baseline"] = {
+                "value": round(rate, 3), "unit": "images/s", "cores": ci["threads"], "kind": "port",
+                "sample": f"{S} images of the same {name} workload, oracle/kpd_oracle.py (dual head"
+                          f"{', detector glue' if detect else ''}), 1 warmup + median of {len(ts)} runs",
+                "cpu_model": ci["model"]}
+            line["gpu_vs_cpu"] = round(line["images_per_s"] / rate, 1)
+            gk = out["keypoints"][:S].cpu()
+            line["parity"] = {"max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
+                              "max_abs_dkh_kpt": float((out["kh_keypoints"][:S].cpu() - ref["kh_keypoints"]).abs().max()),
+                              "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
+                              "images": S}
+        print(json.dumps(line), flush=True)
         del m, img, batch, out
         torch.cuda.empty_cache()
 
