@@ -209,6 +209,10 @@ struct kpd_plan {
   int streams = 1;                        // requested sub-batch streams (kpd_plan_set_streams)
   hipStream_t sub_st[kMaxSub] = {};       // [0] unused: sub-batch 0 runs on the caller's stream
   hipEvent_t fork_ev = nullptr, join_ev[kMaxSub] = {};
+  // pipelined sub-batches (KPD_PIPE): sub-batch k+1 starts when sub-batch k
+  // passes a stage mark, so its latency-bound body overlaps k's heavy stages
+  hipEvent_t pipe_ev[kMaxSub] = {};
+  hipStream_t sub_st_pri[kMaxSub] = {};   // high-priority sub-batch streams (KPD_PIPE_PRI)
   std::map<std::string, std::pair<const void*, size_t>> debug;
   unsigned long long* stamps = nullptr;   // KPD_STAMPS diagnostic buffer (kStampWords)
   // per-stage HIP-event timing (kpd_plan_timing)
@@ -786,6 +790,8 @@ void kpd_plan_destroy(kpd_plan* p) {
   for (int k = 0; k < kpd_plan::kMaxSub; ++k) {
     if (p->sub_st[k]) (void)hipStreamDestroy(p->sub_st[k]);
     if (p->join_ev[k]) (void)hipEventDestroy(p->join_ev[k]);
+    if (p->sub_st_pri[k]) (void)hipStreamDestroy(p->sub_st_pri[k]);
+    if (p->pipe_ev[k]) (void)hipEventDestroy(p->pipe_ev[k]);
   }
   if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
   for (auto& kv : p->timers)
@@ -1189,8 +1195,15 @@ static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts,
 // sub-batch's first image.  Debug buffers are recorded only when debug != 0.
 static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B, int C, int H, int W, float* boxes,
                        int NB, int P, int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis,
-                       float* box_scores, int32_t* topk_out, hipStream_t st) {
+                       float* box_scores, int32_t* topk_out, hipStream_t st, hipEvent_t mark_ev = nullptr,
+                       int mark_at = 0) {
   const bool detect = flags & KPD_FLAG_DETECT, dual = flags & KPD_FLAG_DUAL_HEAD;
+  // pipelined sub-batches: mark_ev is recorded once this sub-batch has passed
+  // stage mark_at (1 body, 2 FPN laterals, 3 FPN level 0, 4 top-k, 5 ROI align)
+  auto mark = [&](int at) -> int {
+    if (mark_ev && mark_at == at) HIP_TRY(hipEventRecord(mark_ev, st));
+    return KPD_OK;
+  };
   Dims d;
   d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P; d.flags = flags;
   d.h[0] = (H - 1) / 2 + 1; d.w[0] = (W - 1) / 2 + 1;
@@ -1376,6 +1389,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       return rc;
   taps[3] = w.last;
   body_stage.reset();
+  if (int rc = mark(1)) return rc;
 
   // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
   const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
@@ -1402,6 +1416,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       return rc;
   }
   lat_stage.reset();
+  if (int rc = mark(2)) return rc;
   std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
   if (lin) {
     Fpn0xArgs a{};
@@ -1427,6 +1442,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     return rc;
   }
   fpn_stage.reset();
+  if (int rc = mark(3)) return rc;
   std::unique_ptr<Stage> topk_stage(new Stage(p, "topk", st));
   if (!p->has_ca) return KPD_OK;   // backbone-only plan (kpd_backbone)
   if (!d.fused_stats) HIP_TRY(launch_channel_stats(w.feat, B, HWf, 128, d.tiles, w.stats, st));
@@ -1435,6 +1451,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st,
                       slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr));
   topk_stage.reset();
+  if (int rc = mark(4)) return rc;
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
   dbg["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
   dbg["scores"] = {w.scores, sizeof(float) * (size_t)B * 128};
@@ -1469,6 +1486,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     if (!slot_in_topk) HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
   }
+  if (int rc = mark(5)) return rc;
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
   if (int rc = run_heatmap_head(p, w, R, P, heat_out, st, KPD_HEAD_ALL, nullptr,
                                  take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
@@ -1520,7 +1538,7 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   const int S = std::max(1, std::min({p->streams, kpd_plan::kMaxSub, B / kMinSub}));
   const int cap = max_pass_images(H, W);
   const size_t img_sz = (size_t)C * H * W, per_kp = (size_t)P * 17;
-  auto run = [&](int k, bool debug, int b0, int b1, hipStream_t sk) -> int {
+  auto run = [&](int k, bool debug, int b0, int b1, hipStream_t sk, hipEvent_t mev = nullptr, int mat = 0) -> int {
     const int nb = b1 - b0;
     const int npass = (nb + cap - 1) / cap;
     for (int q = 0; q < npass; ++q) {
@@ -1531,27 +1549,42 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
                                cbox > 0 || detect ? off(boxes, (size_t)P * 4) : nullptr, cbox, P, flags,
                                off(kpts, per_kp * 2), off(vis, per_kp * 3), off(heat, per_kp * 3136),
                                off(kh_kpts, per_kp * 2), off(kh_vis, per_kp * 3), off(box_scores, (size_t)P),
-                               topk_out ? topk_out + (size_t)c0 * 64 : nullptr, sk))
+                               topk_out ? topk_out + (size_t)c0 * 64 : nullptr, sk, q + 1 == npass ? mev : nullptr,
+                               mat))
         return rc;
     }
     return KPD_OK;
   };
   if (S == 1) return run(0, true, 0, B, st);
+  // A/B (KPD_PIPE=<stage>): sub-batch k+1 waits until sub-batch k has passed
+  // that stage (1 body .. 5 ROI align) instead of starting at once;
+  // KPD_PIPE_PRI=1 runs sub-batches 1.. on high-priority streams, so their
+  // workgroups are dispatched ahead of the running sub-batch's at every free CU
+  static const int pipe_at = getenv("KPD_PIPE") ? atoi(getenv("KPD_PIPE")) : 0;
+  static const bool pipe_pri = getenv("KPD_PIPE_PRI") != nullptr;
   if (!p->fork_ev) HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   for (int k = 1; k < S; ++k) {
     if (!p->sub_st[k]) HIP_TRY(hipStreamCreateWithFlags(&p->sub_st[k], hipStreamNonBlocking));
     if (!p->join_ev[k]) HIP_TRY(hipEventCreateWithFlags(&p->join_ev[k], hipEventDisableTiming));
+    if (pipe_pri && !p->sub_st_pri[k]) {
+      int lo = 0, hi = 0;
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_TRY(hipStreamCreateWithPriority(&p->sub_st_pri[k], hipStreamNonBlocking, hi));
+    }
   }
+  for (int k = 0; k < S && pipe_at > 0; ++k)
+    if (!p->pipe_ev[k]) HIP_TRY(hipEventCreateWithFlags(&p->pipe_ev[k], hipEventDisableTiming));
   HIP_TRY(hipEventRecord(p->fork_ev, st));
   int rc = KPD_OK;
   for (int k = 0; k < S && rc == KPD_OK; ++k) {
     const int b0 = (int)((long)B * k / S), b1 = (int)((long)B * (k + 1) / S);
-    hipStream_t sk = k ? p->sub_st[k] : st;
+    hipStream_t sk = k ? (pipe_pri ? p->sub_st_pri[k] : p->sub_st[k]) : st;
     if (k) HIP_TRY(hipStreamWaitEvent(sk, p->fork_ev, 0));
-    rc = run(k, false, b0, b1, sk);
+    if (k && pipe_at > 0) HIP_TRY(hipStreamWaitEvent(sk, p->pipe_ev[k - 1], 0));
+    rc = run(k, false, b0, b1, sk, pipe_at > 0 && k + 1 < S ? p->pipe_ev[k] : nullptr, pipe_at);
   }
   for (int k = 1; k < S; ++k) {
-    HIP_TRY(hipEventRecord(p->join_ev[k], p->sub_st[k]));
+    HIP_TRY(hipEventRecord(p->join_ev[k], pipe_pri ? p->sub_st_pri[k] : p->sub_st[k]));
     HIP_TRY(hipStreamWaitEvent(st, p->join_ev[k], 0));
   }
   return rc;

@@ -139,6 +139,7 @@ class MultiPersonKeypointModel(nn.Module):
         self.streams = streams          # sub-batch streams for B >= 32 (kpd_plan_set_streams)
         self._plan: Optional[_native.Plan] = None
         self._plan_key = None
+        self._plan_streams: Optional[int] = None
         self._state_tensors: Optional[List[torch.Tensor]] = None
         if config.num_keypoints != 17 or config.heatmap_head.in_channels != 64 \
                 or config.backbone.out_channels != 128:
@@ -154,7 +155,7 @@ class MultiPersonKeypointModel(nn.Module):
             self._state_tensors = list(self.state_dict(keep_vars=True).values())
         vers = tuple((t.data_ptr(), t._version) for t in self._state_tensors)
         ph = self.config.person_head
-        return (device, self.precision, self.streams, ph.conf_threshold, ph.nms_iou_threshold, vers)
+        return (device, self.precision, ph.conf_threshold, ph.nms_iou_threshold, vers)
 
     def _apply(self, fn, *args, **kwargs):
         self._state_tensors = None
@@ -175,8 +176,10 @@ class MultiPersonKeypointModel(nn.Module):
             plan.finalize(_native.PRECISIONS[self.precision])
             ph = self.config.person_head
             plan.set_detector(ph.conf_threshold, ph.nms_iou_threshold)
-            plan.set_streams(self.streams)
-            self._plan, self._plan_key = plan, key
+            self._plan, self._plan_key, self._plan_streams = plan, key, None
+        if self._plan_streams != self.streams:   # a scheduling setting: no re-pack of the weights
+            self._plan.set_streams(self.streams)
+            self._plan_streams = self.streams
         return self._plan
 
     def invalidate_plan(self) -> None:
