@@ -92,6 +92,54 @@ __global__ __launch_bounds__(256) void kh_att_kernel(float* __restrict__ x, cons
   }
 }
 
+// Split-operand variant (KEYPOINT_HEAD on hmconv_kernel, MODE 2): the same
+// x * att (fp32), scaled by ROI r's power of two and written as f16 hi + lo in
+// [hi32 | lo32] groups at the padded position (y + 1, x + 1) of the ROI's 58x58
+// map (the zero border is never written).  |x * att| <= |x| <= bound: the
+// scale 2^a, a = split_exp_of(bound), keeps hi below 2^15; the first conv's
+// input unscale reads the same bound from hsc[r][2].
+__global__ __launch_bounds__(256) void kh_att_split_kernel(const float* __restrict__ x, const float* __restrict__ sa1,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           const float* __restrict__ bound, int bdiv, int bstride,
+                                                           float* __restrict__ hsc, int R, _Float16* __restrict__ out) {
+  __shared__ float sw[64];
+  if (threadIdx.x < 64) sw[threadIdx.x] = w[threadIdx.x];
+  __syncthreads();
+  const size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (size_t)R * GP) return;
+  const int r = (int)(pix / GP), rem = (int)(pix - (size_t)r * GP), yy = rem / G, xx = rem - yy * G;
+  const float4* s = reinterpret_cast<const float4*>(sa1 + pix * 64);
+  float a = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 v = s[q];
+    a = fmaf(sw[4 * q], v.x, a); a = fmaf(sw[4 * q + 1], v.y, a);
+    a = fmaf(sw[4 * q + 2], v.z, a); a = fmaf(sw[4 * q + 3], v.w, a);
+  }
+  const float att = kpd_sigmoid(a + b[0]);
+  const float bnd = bound[(size_t)(r / bdiv) * bstride];
+  if (rem == 0) hsc[(size_t)r * 4 + 2] = bnd;
+  const float sc = ldexpf(1.f, split_exp_of(bnd));
+  const float4* xp = reinterpret_cast<const float4*>(x + pix * 128);
+  _Float16* o = out + (((size_t)r * (G + 2) + yy + 1) * (G + 2) + xx + 1) * 256;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+  for (int q8 = 0; q8 < 16; ++q8) {   // 8 channels per step: one 16-byte hi and lo store each
+    const float4 u0 = xp[2 * q8], u1 = xp[2 * q8 + 1];
+    const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    h8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xs = (v[e] * att) * sc;
+      hi[e] = (_Float16)xs;
+      lo[e] = (_Float16)(xs - (float)hi[e]);
+    }
+    const int c = q8 * 8;
+    *reinterpret_cast<h8*>(o + (c / 32) * 64 + c % 32) = hi;
+    *reinterpret_cast<h8*>(o + (c / 32) * 64 + 32 + c % 32) = lo;
+  }
+}
+
 // adaptive avg pool of an NHWC [R][56][56][C] map to (o x o), written in
 // NCHW-flatten order (c*o*o + y*o + x) as nn.Flatten after the pool does.
 // grid R, 256 threads over (c, y, x) outputs.
@@ -183,6 +231,16 @@ hipError_t launch_person_decode(const float* head, int B, int hc, const float* a
 
 hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st) {
   hipLaunchKernelGGL(kh_att_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, x, sa1, w, b, npix);
+  return hipGetLastError();
+}
+
+hipError_t launch_kh_att_split(const float* x, const float* sa1, const float* w, const float* b, int R,
+                               const float* bound, int bdiv, int bstride, float* hsc, void* out, hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  if (!bound || bdiv < 1 || bstride < 1 || !hsc || !out) return hipErrorInvalidValue;
+  const size_t n = (size_t)R * GP;
+  hipLaunchKernelGGL(kh_att_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, sa1, w, b, bound,
+                     bdiv, bstride, hsc, R, static_cast<_Float16*>(out));
   return hipGetLastError();
 }
 

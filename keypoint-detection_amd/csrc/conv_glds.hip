@@ -1044,10 +1044,21 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // registers to spare; the BN = 256 tiles have no room for a second set).
 // NW: waves per workgroup (8; 4 for conv 3: 64 x 64 wave tiles, 1.5x fewer
 // LDS fragment bytes per MFMA than 8 waves of 32 x 64, one wave per SIMD).
+// MODE: epilogue -- 0 bias + ReLU, re-split (or bf16) for the next conv; 1 the
+// fused final 1x1 + sigmoid (heatmap); 2 KEYPOINT_HEAD (keypoint_head.py:
+// 64-90): bias + ReLU6, the ResidualBlock's bn1 affine + ReLU6, the
+// downsample residual + ReLU6, outputs split (next conv) and / or fp32 (pools).
+// -1: 1 for BN = 64, else 0.
+// NTAP (MODE 2): 10 = the 3x3 taps plus the ResidualBlock's 1x1 downsample as
+// a tenth K-step per chunk (the centre tap's A rows, its own weights) into a
+// second accumulator set.
 template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false,
-          int NW = 8>
+          int NW = 8, int MODE = -1, int NTAP = 9>
 __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   constexpr int NTH = NW * 64;
+  constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
+  static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB && TPS == 1), "tenth tap: KH downsample");
+  static_assert(EMODE != 2 || (SPLIT && !DB && TPS == 1), "KH epilogue: split, one tap per K-step");
   constexpr int WAVES_N = BN / 64, WAVES_M = NW / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
   static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
@@ -1057,20 +1068,22 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
   constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
   static_assert(TPS == 1 || (SPLIT && 9 % TPS == 0), "taps per step");
-  constexpr bool FINAL = BN == 64;
-  constexpr int EPI = FINAL ? 0 : epi_lds_bytes<BMH, 128, NTH>();
+  constexpr bool FINAL = EMODE == 1;
+  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH, 128, NTH>();
   constexpr int LDS = RING > EPI ? RING : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  // KH mode: column groups by wave halves (waves w and w + 4 share a SIMD, so
+  // a group with fewer live columns pairs with a full one on every SIMD)
+  const int wm = EMODE == 2 ? wave % WAVES_M : wave / WAVES_N, wn = EMODE == 2 ? wave / WAVES_M : wave % WAVES_N;
   const int NTL = p.cout / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = HP + p.m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
   // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
   // channels as [hi32 | lo32] f16
-  const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = 9 * NC;
+  const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = NTAP * NC;
   stamp16(p.stamps, 0);
   const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
@@ -1086,7 +1099,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
   for (int i = 0; i < B_LD; ++i) {
     const int co = n0 + wave * (BN / NW) + i * 8 + lrow;
-    b_off[i] = (unsigned)(co * 9 * RB + lchunk * 16);
+    b_off[i] = (unsigned)(co * NTAP * RB + lchunk * 16);
   }
   auto issue_a = [&](int c, int i) {   // A window of chunk c, wave-instruction i
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / NW) + i * 8) * ROWB);
@@ -1095,7 +1108,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   auto issue_b = [&](int k) {          // B of K-step k (TPS taps of one chunk) into stage k % SB
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
-      const int sk = k * TPS + u, c = sk / 9, t = sk - c * 9;
+      const int sk = k * TPS + u, c = sk / NTAP, t = sk - c * NTAP;
       const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + u * BN * ROWB +
                                                           wave * (BN / NW) * ROWB);
 #pragma unroll
@@ -1117,11 +1130,11 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
     asm volatile("" ::: "memory");
   };
 
-  f32x4 acc[FM][FN];
+  f32x4 acc[FM][FN], acc2[FM][FN];   // acc2: the downsample (NTAP 10)
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, r16 = lane & 15;
   const int b_row = (wn * 64 + r16) * ROWB;
   const int bch0 = ((g ^ (r16 & 7)) << 4), bch1 = (((4 + g) ^ (r16 & 7)) << 4);
@@ -1191,7 +1204,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   // the next chunk's window, spread over this chunk's K-steps: pieces of
   // K-step k1 (TPS = 1: piece t1 at taps 0-5; else an equal share per step)
   auto issue_a_at = [&](int k1) {
-    const int s1 = k1 * TPS, c1 = s1 / 9, jj = (s1 - c1 * 9) / TPS;
+    const int s1 = k1 * TPS, c1 = s1 / NTAP, jj = (s1 - c1 * NTAP) / TPS;
     if (c1 + 1 >= NC) return;
     if constexpr (TPS == 1) {
       if (jj < A_LD) issue_a(c1 + 1, jj);
@@ -1245,26 +1258,21 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
     // read bh' | P3 ah.bl | read ah', bl'.
     uint4 ah[FM], al[FM], bh[FN], bl[FN];
     auto rd_a = [&](int k, int q, uint4* f) {
-      const int c = k / 9, t = k - c * 9, off = (t / 3 - 1) * HP + (t % 3 - 1);
+      const int c = k / NTAP, t = k - c * NTAP, off = t == 9 ? 0 : (t / 3 - 1) * HP + (t % 3 - 1);
       const char* ab = lds + (c & 1) * ABUF;
       const int r0w = wm * WM + r16 + 64 + off;
       const int ach = (((q ? 4 : 0) + g) ^ (r0w & 7)) << 4;
 #pragma unroll
       for (int i = 0; i < FM; ++i) f[i] = *reinterpret_cast<const uint4*>(ab + (r0w + i * 16) * ROWB + ach);
     };
-    auto rd_b = [&](int k, int q, uint4* f) {   // k: tap sub-step
-      const char* bb = lds + 2 * ABUF + ((k / TPS) % SB) * BSTAGE + (k % TPS) * BN * ROWB;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
-    };
     // stagger (HmConvArgs::stagger): waves 4-7 issue a barrier's DMA pieces
     // after pass 2 instead of right after the barrier, so one wave of each
     // SIMD pair issues while its partner's MFMAs run (conv 1 / 2 K step
     // 1.84 / 1.81 -> 1.75 / 1.77 us)
     const bool late = p.stagger && __builtin_amdgcn_readfirstlane(wave) >= 4;
-    auto pass = [&](const uint4* a, const uint4* b) {
+    auto pass = [&](f32x4 (&A)[FM][FN], const uint4* a, const uint4* b) {
       if constexpr ((DBG & 1) != 0) {
-        acc[0][0][0] += __uint_as_float(a[0].x ^ b[FN - 1].w);
+        A[0][0][0] += __uint_as_float(a[0].x ^ b[FN - 1].w);
         return;
       }
       __builtin_amdgcn_s_setprio(1);
@@ -1272,8 +1280,8 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, b[j]),
-                                                             acc[i][j], 0, 0, 0);
+          A[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]), __builtin_bit_cast(f16x8, b[j]),
+                                                           A[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     };
     if constexpr (DB) {
@@ -1311,7 +1319,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
           const int cc = c + tt / 9, t = tt % 9, k = cc * 9 + t;
           Frag& cur = (tt & 1) ? f1 : f0;
           Frag& nxt = (tt & 1) ? f0 : f1;
-          pass(cur.al, cur.bh);
+          pass(acc, cur.al, cur.bh);
           const bool kstep = k + 1 < KT && (t + 1) % TPS == 0;
           if (k + 1 < KT) {
             const int tn = (tt + 1) % 18, cn = c + (tt + 1) / 9;   // next sub-step (chunk cn, tap tn % 9)
@@ -1323,35 +1331,98 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
             // stage of the next sub-step: (its K-step) % 2 = (tn / 9 + (tn % 9) / TPS) % 2 with c even
             rd_all(cn, tn % 9, ((tn / 9) * (9 / TPS) + (tn % 9) / TPS) & 1, nxt);
           }
-          pass(cur.ah, cur.bh);
+          pass(acc, cur.ah, cur.bh);
           if (kstep && late) issue_at((k + 1) / TPS);
-          pass(cur.ah, cur.bl);
+          pass(acc, cur.ah, cur.bl);
         }
       }
     } else {
-    rd_a(0, 1, al);
-    rd_b(0, 0, bh);
-    rd_a(0, 0, ah);
-    rd_b(0, 1, bl);
-    for (int k = 0; k < KT; ++k) {   // tap sub-steps; a barrier where a K-step begins
-      const bool more = k + 1 < KT, kstep = more && (k + 1) % TPS == 0;
-      pass(al, bh);
-      if (more) {
-        if (kstep) {
-          const int k1 = (k + 1) / TPS;
-          barrier_k(k1 + SB - 2 >= KS);   // B(k1) and its chunk's window landed; reads of k1 - 1 retired
-          if (!late) issue_at(k1);
+    // The K loop with NB_ weight fragments read per step and NM_ / NM9_ of
+    // them multiplied (taps 0-8 / the downsample tap): KH mode skips the
+    // fragments of its zero-padded columns (wave-uniform counts); elsewhere all FN.
+    auto run_loop = [&](auto NBc, auto NMc, auto NM9c) {
+      constexpr int NB_ = decltype(NBc)::value;
+      auto rd_bn = [&](int k, int q, uint4* f) {
+        const char* bb = lds + 2 * ABUF + ((k / TPS) % SB) * BSTAGE + (k % TPS) * BN * ROWB;
+#pragma unroll
+        for (int j = 0; j < NB_; ++j)
+          f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
+      };
+      auto passn = [&](f32x4 (&A)[FM][FN], const uint4* a, const uint4* b, auto NMx) {
+        constexpr int NM_ = decltype(NMx)::value;
+        if constexpr (NM_ == FN) {
+          pass(A, a, b);
+        } else if constexpr (NM_ > 0) {
+          if constexpr ((DBG & 1) != 0) {
+            A[0][0][0] += __uint_as_float(a[0].x ^ b[0].w);
+            return;
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < NM_; ++j)
+              A[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[i]),
+                                                               __builtin_bit_cast(f16x8, b[j]), A[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
         }
-        rd_a(k + 1, 1, al);
+      };
+      rd_a(0, 1, al);
+      rd_bn(0, 0, bh);
+      rd_a(0, 0, ah);
+      rd_bn(0, 1, bl);
+      // tap sub-step k into the accumulator set A; a barrier where a K-step begins
+      auto sub = [&](int k, f32x4 (&A)[FM][FN], auto NMx) {
+        const bool more = k + 1 < KT, kstep = more && (k + 1) % TPS == 0;
+        passn(A, al, bh, NMx);
+        if (more) {
+          if (kstep) {
+            const int k1 = (k + 1) / TPS;
+            barrier_k(k1 + SB - 2 >= KS);   // B(k1) and its chunk's window landed; reads of k1 - 1 retired
+            if (!late) issue_at(k1);
+          }
+          rd_a(k + 1, 1, al);
+        }
+        passn(A, ah, bh, NMx);
+        if (kstep && late) issue_at((k + 1) / TPS);
+        if (more) rd_bn(k + 1, 0, bh);
+        passn(A, ah, bl, NMx);
+        if (more) {
+          rd_a(k + 1, 0, ah);
+          rd_bn(k + 1, 1, bl);
+        }
+      };
+      if constexpr (NTAP == 10) {
+        for (int c = 0; c < NC; ++c) {
+          for (int t = 0; t < 9; ++t) sub(c * NTAP + t, acc, NMc);
+          sub(c * NTAP + 9, acc2, NM9c);   // the 1x1 downsample: centre-tap rows, its own weights
+        }
+      } else {
+        for (int k = 0; k < KT; ++k) sub(k, acc, NMc);
       }
-      pass(ah, bh);
-      if (kstep && late) issue_at((k + 1) / TPS);
-      if (more) rd_b(k + 1, 0, bh);
-      pass(ah, bl);
-      if (more) {
-        rd_a(k + 1, 0, ah);
-        rd_b(k + 1, 1, bl);
+    };
+    using IFN = std::integral_constant<int, FN>;
+    if constexpr (EMODE == 2) {
+      // live fragments of this wave's columns: [0, ns + nf) for the 3x3 taps,
+      // [0, ns) (the ResidualBlock columns) for the downsample tap
+      const int c0 = __builtin_amdgcn_readfirstlane(n0 + wn * 64);
+      const int nact = min(max((p.ns + p.nf - c0 + 15) / 16, 0), FN), nact9 = min(max((p.ns - c0 + 15) / 16, 0), FN);
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      // the column plans in use (launch_hmconv_kh): [64 + ds | 32 + 32 zero] at
+      // BN 128, [32 + ds | 32 zero] and [16 | 48 zero] at BN 64
+      if (BN == 128 && nact == 2 && nact9 == 0) {
+        if constexpr (BN == 128) run_loop(I2{}, I2{}, I0{});
+      } else if (BN == 64 && NTAP == 10 && nact == 2 && nact9 == 2) {
+        if constexpr (BN == 64 && NTAP == 10) run_loop(I2{}, I2{}, I2{});
+      } else if (BN == 64 && NTAP == 9 && nact == 1) {
+        if constexpr (BN == 64 && NTAP == 9) run_loop(I1{}, I1{}, I1{});
+      } else {
+        run_loop(IFN{}, IFN{}, IFN{});
       }
+    } else {
+      run_loop(IFN{}, IFN{}, IFN{});
     }
     }
   }
@@ -1367,7 +1438,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
     xx = rem - (yy + 1) * HP - 1;
     return m < Mtot - HP && yy >= 0 && yy < HP - 2 && xx >= 0 && xx < HP - 2;
   };
-  if constexpr (!FINAL) {
+  if constexpr (EMODE == 0) {
     // bias + ReLU through the LDS tile (two 128-column halves): bf16 16-byte
     // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
     // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
@@ -1425,7 +1496,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
         }
       }
     }
-  } else {
+  } else if constexpr (EMODE == 1) {
     // conv 3 (64 channels, bias + ReLU) -> final 1x1 64->17 + sigmoid per pixel
     constexpr int NKF = 17;
     float* fw = reinterpret_cast<float*>(lds);
@@ -1496,6 +1567,66 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
         if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? sigmoid_rcp(val + fw[NKF * 64 + k]) : 0.f;
       }
     }
+  } else {
+    // KEYPOINT_HEAD (keypoint_head.py:64-90, :25-27, :38-40), per output column co:
+    //   v = relu6(conv * u + b[co]); v = relu6(v * ps[co] + pt[co])   (ResidualBlock.bn1; 1, 0 elsewhere)
+    //   NTAP 10: v = relu6(v + downsample * u + bd[co])               (identity branch)
+    // columns [0, ns) -> the next conv's split operand (padded map, scale os);
+    // [ns, ns + nf) -> fp32 [R][56][56][nf] (adaptive-pool inputs); beyond: padding.
+    // A DPP quad transpose gives each lane 4 consecutive columns of one row.
+    const int t4 = lane & 3, q4 = r16 >> 2;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        quad_transpose(acc[i][j], t4);
+        if constexpr (NTAP == 10) quad_transpose(acc2[i][j], t4);
+      }
+    auto relu6 = [](float x) { return fminf(fmaxf(x, 0.f), 6.f); };
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = n0 + wn * 64 + j * 16 + q4 * 4;
+      if (co >= p.ns + p.nf) continue;
+      const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+      const float4 ps = *reinterpret_cast<const float4*>(p.kh_ps + co);
+      const float4 pt = *reinterpret_cast<const float4*>(p.kh_pt + co);
+      float4 bd = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (NTAP == 10) bd = *reinterpret_cast<const float4*>(p.kh_bd + co);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, sv[4] = {ps.x, ps.y, ps.z, ps.w}, tv[4] = {pt.x, pt.y, pt.z, pt.w};
+      const float dv[4] = {bd.x, bd.y, bd.z, bd.w};
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * WM + i * 16 + g * 4 + t4;
+        int r, yy, xx;
+        if (!interior(m, r, yy, xx)) continue;
+        const int q = m >= rbound;
+        const float u = q ? us[1] : us[0];
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = relu6(fmaf(acc[i][j][e], u, bv[e]));
+          x = relu6(fmaf(x, sv[e], tv[e]));
+          if constexpr (NTAP == 10) x = relu6(x + fmaf(acc2[i][j][e], u, dv[e]));
+          o[e] = x;
+        }
+        if (co < p.ns) {
+          const float sc = q ? os[1] : os[0];
+          f16x4 hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xs = o[e] * sc;
+            hi[e] = (_Float16)xs;
+            lo[e] = (_Float16)(xs - (float)hi[e]);
+          }
+          char* ob = static_cast<char*>(p.out) + (size_t)m * (p.ns * 4) + (co >> 5) * 128 + (co & 31) * 2;
+          *reinterpret_cast<f16x4*>(ob) = hi;
+          *reinterpret_cast<f16x4*>(ob + 64) = lo;
+        } else {
+          *reinterpret_cast<float4*>(p.outf + ((size_t)r * (HP - 2) * (HP - 2) + yy * (HP - 2) + xx) * p.nf +
+                                     (co - p.ns)) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
   }
   if (p.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1554,8 +1685,46 @@ hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream
   return hipErrorInvalidValue;
 }
 
+// KEYPOINT_HEAD convs (MODE 2): cin 128 / 64 / 32 (compile-time), cout 128 or
+// 64 (one column tile), the downsample as a tenth tap or not
+static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
+  if (!a0.split || !a0.hsc || a0.in_idx < 0 || a0.in_idx > 3 || (a0.ns > 0 && (!a0.out || a0.out_idx < 0 ||
+      a0.out_idx > 3 || a0.ns % 32)) || (a0.nf > 0 && !a0.outf) || a0.nf % 16 || a0.ns + a0.nf > a0.cout ||
+      (a0.ntap != 9 && a0.ntap != 10) || (a0.ntap == 10 && !a0.kh_bd) || !a0.kh_pt || !a0.bias)
+    return hipErrorInvalidValue;
+  const int sel = (a0.cin == 128 && a0.cout == 128 && a0.ntap == 10) ? 1
+                : (a0.cin == 64 && a0.cout == 64 && a0.ntap == 10) ? 2
+                : (a0.cin == 32 && a0.cout == 64 && a0.ntap == 9) ? 3 : 0;
+  if (!sel) return hipErrorInvalidValue;
+  HmConvArgs a = a0;
+  const long wt_bytes = (long)a.cout * a.ntap * a.cin * 4, roi_bytes = (long)HPP * a.cin * 4;
+  if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
+  a.wt_bytes = (int)wt_bytes;
+  a.m_off = 0;
+  a.stagger = 0;
+  const int chunk = (int)std::min<long>(a0.R, kMaxDesc / roi_bytes);
+  for (int r0 = 0; r0 < a0.R; r0 += chunk) {
+    const int nr = std::min(chunk, a0.R - r0);
+    a.R = nr;
+    a.r0 = a0.r0 + r0;
+    a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
+    if (a0.out) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.ns * 4;
+    if (a0.outf) a.outf = a0.outf + (size_t)r0 * (HP - 2) * (HP - 2) * a.nf;
+    a.in_bytes = (int)(nr * roi_bytes);
+    const long rows = (long)nr * HPP - 2 * HP;
+    const dim3 grid((unsigned)((rows + BM - 1) / BM));
+    if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 3, 0, BM, true, 128, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+    else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 32, 1, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
   if (a0.R <= 0) return hipSuccess;
+  if (a0.kh_ps) return launch_hmconv_kh(a0, st);
   const bool fin = a0.fin_w != nullptr, split = a0.split != 0;
   if (a0.cin % (split ? 32 : 64) || (fin ? a0.cout != 64 : a0.cout % 128) ||
       (fin && (!a0.slot || !a0.heat || !a0.fin_b)) || (!fin && !a0.out) ||

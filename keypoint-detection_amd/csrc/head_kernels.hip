@@ -37,7 +37,8 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
                                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                                    const float* __restrict__ w2, const float* __restrict__ b2,
                                                    int32_t* __restrict__ topk, float* __restrict__ scores_out,
-                                                   const float* __restrict__ boxes, int P, int32_t* __restrict__ slot) {
+                                                   const float* __restrict__ boxes, int P, int32_t* __restrict__ slot,
+                                                   float* __restrict__ imax) {
   extern __shared__ __attribute__((aligned(16))) float tsm[];
   // more tiles than fit in LDS (the fp32 path's small tiles at 384x288):
   // the partials are summed straight from global memory
@@ -96,6 +97,14 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
     // (optional) the image's box slot map (slotmap_kernel's work) on a thread
     // of the otherwise idle upper waves: one launch less per forward
     if (slot && c == 255) slotmap_image(boxes, n, P, slot);
+    // (optional) the image's max over FPN level 0 (its channel maxima; the map
+    // follows a ReLU, so this is max |x|): the bound of the KEYPOINT_HEAD's
+    // split operand, whose ROI features interpolate this map
+    if (imax && c == 128) {
+      float M = 0.f;
+      for (int k = 0; k < FC; ++k) M = fmaxf(M, mx[k]);
+      imax[n] = M;
+    }
     return;
   }
   float oa = b2[c], om = b2[c];
@@ -608,11 +617,11 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
 
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
-                       const float* boxes, int P, int32_t* slot) {
+                       const float* boxes, int P, int32_t* slot, float* imax) {
   if (slot && (!boxes || P <= 0 || P > 0xFFFF)) return hipErrorInvalidValue;
   const size_t lds = ((size_t)(tiles <= kTopkMaxTiles ? tiles : 0) * 2 * FC + 2 * 8 * FC) * 4;
   hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores,
-                     boxes, P, slot);
+                     boxes, P, slot, imax);
   return hipGetLastError();
 }
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipStream_t st) {

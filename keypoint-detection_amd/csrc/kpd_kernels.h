@@ -84,6 +84,14 @@ struct HmConvArgs {
   int in_bytes, wt_bytes;   // launcher
   int stagger;              // launcher: split K loop, waves 4-7 issue their DMA one pass later
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
+  // KEYPOINT_HEAD mode (kh_ps != null; split only): wt is [cout][ntap][cin] with
+  // ntap = 10 when the ResidualBlock's 1x1 downsample rides along as a tenth
+  // tap; per column co: v = relu6(acc + bias), v = relu6(v * kh_ps + kh_pt),
+  // (ntap 10) v = relu6(v + downsample + kh_bd); columns [0, ns) -> out (split,
+  // [R][58][58][ns]), [ns, ns + nf) -> outf fp32 [R][56][56][nf]
+  const float *kh_ps, *kh_pt, *kh_bd;
+  float* outf;
+  int ns, nf, ntap;
 };
 hipError_t launch_hmconv(const HmConvArgs& a, hipStream_t st);
 constexpr int kHmPad = 58;   // padded ROI side of the hmconv layout
@@ -242,7 +250,7 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
 // slot != nullptr: also writes the slot map of boxes [N][P][4] (launch_slotmap's work)
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
-                       const float* boxes = nullptr, int P = 0, int32_t* slot = nullptr);
+                       const float* boxes = nullptr, int P = 0, int32_t* slot = nullptr, float* imax = nullptr);
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
@@ -281,6 +289,11 @@ hipError_t launch_adaptive_pool56(const float* in, int B, int Hf, int Wf, int C,
 hipError_t launch_person_decode(const float* head, int B, int hc, const float* anchors, int img_h, int img_w,
                                 float conf, float* cand_boxes, float* cand_scores, hipStream_t st);
 hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st);
+// the attention-weighted KEYPOINT_HEAD input as the split operand of the first
+// hmconv (KH mode): [R][58][58][128] f16 [hi32 | lo32], ROI r scaled by
+// 2^split_exp_of(bound[(r / bdiv) * bstride]), which is also stored to hsc[r][2]
+hipError_t launch_kh_att_split(const float* x, const float* sa1, const float* w, const float* b, int R,
+                               const float* bound, int bdiv, int bstride, float* hsc, void* out, hipStream_t st);
 hipError_t launch_kh_pool(const float* in, int R, int C, int o, float* out, int out_stride, hipStream_t st);
 hipError_t launch_kh_final(const float* lin_r, int r_stride, const float* lin_v, int v_stride, const float* ln_rg,
                            const float* ln_rb, const float* w_r, const float* b_r, const float* ln_vg,

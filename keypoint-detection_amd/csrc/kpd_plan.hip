@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <memory>
 #include <string>
@@ -101,6 +102,16 @@ struct DevBneck {
   DevSE se;
 };
 
+// KEYPOINT_HEAD conv as a split hmconv (MODE 2): several convs' columns side
+// by side, f16 [cout][ntap][cin] [hi32 | lo32] weights scaled 2^w_exp, per
+// column bias / second affine (ps, pt) / downsample bias (bd)
+struct KhSplit {
+  void* ws = nullptr;
+  int w_exp = 0;
+  float *b = nullptr, *ps = nullptr, *pt = nullptr, *bd = nullptr;
+  int cin = 0, cout = 0, ntap = 9, ns = 0, nf = 0;
+};
+
 struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* stem = nullptr;
   float* e[11] = {};
@@ -141,6 +152,11 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   // KEYPOINT_HEAD
   float *kx = nullptr, *ksa = nullptr, *kds1 = nullptr, *krb1 = nullptr, *kds2 = nullptr, *krb2 = nullptr;
   float *kr3 = nullptr, *kv1 = nullptr, *kpr = nullptr, *kpv = nullptr, *klr = nullptr, *klv = nullptr;
+  // KEYPOINT_HEAD on the split hmconv path: zero-bordered [R][58][58][C] f16
+  // [hi32 | lo32] operands (x * att, ResidualBlock 1 / 2 outputs) and the
+  // per-image FPN level-0 maximum (their scale bound, written by topk_kernel)
+  void *kxs = nullptr, *kr1s = nullptr, *kr2s = nullptr;
+  float* imax = nullptr;
 };
 
 struct Dims {
@@ -198,6 +214,11 @@ struct kpd_plan {
   float *kh_bn1a_s = nullptr, *kh_bn1a_t = nullptr, *kh_bn1b_s = nullptr, *kh_bn1b_t = nullptr;
   float *kh_lnr_g = nullptr, *kh_lnr_b = nullptr, *kh_fr_w = nullptr, *kh_fr_b = nullptr;
   float *kh_lnv_g = nullptr, *kh_lnv_b = nullptr, *kh_fv_w = nullptr, *kh_fv_b = nullptr;
+  // split (fp32-accurate) KEYPOINT_HEAD convs on hmconv_kernel: [ResidualBlock 1
+  // (+ downsample tap) | visibility conv], [ResidualBlock 2 (+ downsample)],
+  // [regression 3x3]; kh_split = all three packed (split / mixed precision)
+  KhSplit kh_s[3];
+  bool kh_split = false;
   // workspace, one per concurrent sub-batch (kpd_plan_set_streams)
   static constexpr int kMaxSub = 4;
   static constexpr int kOpWs = kMaxSub;   // workspace of the stand-alone operator entry points
@@ -435,6 +456,71 @@ int pack_split_1x1(kpd_plan* p, DevConv& dc) {
   return KPD_OK;
 }
 
+// KEYPOINT_HEAD convs for hmconv_kernel MODE 2 (keypoint_head.py:22-48,
+// 64-90): the parts' output columns side by side from column `col`, taps 0-8
+// their 3x3 weights (BN folded), tap 9 (ntap 10) the ResidualBlock's 1x1
+// downsample (BN folded) for its own columns, zero elsewhere; columns beyond
+// the parts are zero padding.  Per column: bias, the ResidualBlock.bn1 affine
+// (ps, pt; 1 and 0 for plain conv + BN + ReLU6 columns) and the downsample
+// bias.  Split into f16 hi + lo after one power-of-two scale (as pack_split_hm).
+struct KhPart { const DevConv* conv; const DevConv* ds; const float* ps; const float* pt; int col; };
+int pack_split_kh(kpd_plan* p, KhSplit& ks, int cin, int cout, int ntap, std::initializer_list<KhPart> parts) {
+  std::vector<float> W((size_t)cout * ntap * cin, 0.f), b(cout, 0.f), ps(cout, 1.f), pt(cout, 0.f), bd(cout, 0.f);
+  for (const KhPart& q : parts) {
+    const DevConv& c = *q.conv;
+    if (c.k != 3 || c.bf16 || c.cin_p != cin || q.col + c.cout > cout) return fail(KPD_EINVAL, "KH split pack: shape");
+    std::vector<float> w((size_t)c.cout_p * 9 * cin), cb(c.cout_p);
+    HIP_TRY(hipMemcpy(w.data(), c.w, w.size() * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cb.data(), c.b, cb.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (int co = 0; co < c.cout; ++co) {
+      for (int t = 0; t < 9; ++t)
+        for (int ci = 0; ci < cin; ++ci)
+          W[((size_t)(q.col + co) * ntap + t) * cin + ci] = w[((size_t)co * 9 + t) * cin + ci];
+      b[q.col + co] = cb[co];
+    }
+    if (q.ps) {
+      std::vector<float> s(c.cout), t(c.cout);
+      HIP_TRY(hipMemcpy(s.data(), q.ps, s.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(t.data(), q.pt, t.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (int co = 0; co < c.cout; ++co) { ps[q.col + co] = s[co]; pt[q.col + co] = t[co]; }
+    }
+    if (q.ds) {
+      const DevConv& d = *q.ds;
+      if (ntap != 10 || d.k != 1 || d.bf16 || d.cin_p != cin || d.cout != c.cout) return fail(KPD_EINVAL, "KH split pack: ds");
+      std::vector<float> dw((size_t)d.cout_p * cin), db(d.cout_p);
+      HIP_TRY(hipMemcpy(dw.data(), d.w, dw.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(db.data(), d.b, db.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (int co = 0; co < d.cout; ++co) {
+        for (int ci = 0; ci < cin; ++ci) W[((size_t)(q.col + co) * ntap + 9) * cin + ci] = dw[(size_t)co * cin + ci];
+        bd[q.col + co] = db[co];
+      }
+    }
+  }
+  float mx = 0.f;
+  for (float v : W) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) std::frexp(mx, &e);
+  const int w_exp = std::min(std::max(14 - e, -100), 100);
+  std::vector<_Float16> hl(2 * W.size());
+  for (size_t row = 0; row < (size_t)cout * ntap; ++row)
+    for (int ci = 0; ci < cin; ++ci) {
+      const float x = std::ldexp(W[row * cin + ci], w_exp);
+      const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+      const size_t o = row * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
+      hl[o] = hi;
+      hl[o + 32] = lo;
+    }
+  _Float16* d = nullptr;
+  if (int rc = upload(p, hl, &d)) return rc;
+  ks.ws = d;
+  ks.w_exp = w_exp;
+  ks.cin = cin; ks.cout = cout; ks.ntap = ntap;
+  if (int rc = upload(p, b, &ks.b)) return rc;
+  if (int rc = upload(p, ps, &ks.ps)) return rc;
+  if (int rc = upload(p, pt, &ks.pt)) return rc;
+  return upload(p, bd, &ks.bd);
+}
+
 // FPN level 0 by linearity (fpn0x_kernel): W0 = W3 . L0 (the 3x3 conv on the
 // 16-channel stem tap through the bias-free lateral 0) and, per output position
 // class (y % 4, x % 4), the 3x3 taps summed by the lateral-1 pixel they read
@@ -587,6 +673,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.separt = c.take<float>((size_t)B * kSePartFloats);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
+  w.imax = c.take<float>((size_t)B);
   if (R > 0) {
     const size_t px = R * 3136;
     const size_t es = p->precision == KPD_PRECISION_MIXED ? 2 : 4;   // bf16, or f16 hi + lo / fp32
@@ -617,6 +704,12 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
       w.kpv = c.take<float>(R * 512);
       w.klr = c.take<float>(R * 256);
       w.klv = c.take<float>(R * 128);
+      if (p->kh_split) {
+        const size_t pp = R * kHmPad * kHmPad;
+        w.kxs = c.take<char>(pp * 128 * 4);
+        w.kr1s = c.take<char>(pp * (size_t)p->kh_s[0].ns * 4);
+        w.kr2s = c.take<char>(pp * (size_t)p->kh_s[1].ns * 4);
+      }
     }
   }
   if (d.flags & KPD_FLAG_DETECT) {
@@ -817,6 +910,8 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   for (auto& c : p->fpn_lv) c = DevConv();
   p->kh_ds1 = DevConv();
   p->kh_ds2 = DevConv();
+  for (auto& k : p->kh_s) k = KhSplit();
+  p->kh_split = false;
   p->has_kh = false;
   for (int k = 0; k <= kpd_plan::kMaxSub; ++k) {
     if (p->ws[k]) { (void)hipFree(p->ws[k]); p->ws[k] = nullptr; p->ws_bytes[k] = 0; }
@@ -1004,6 +1099,21 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
         return fail(KPD_EINVAL, "KEYPOINT_HEAD shape not supported (needs in 128, regression 32, square pool)");
       p->kh_o = o;
     }
+    // split KEYPOINT_HEAD convs (the default channel plan: ResidualBlocks
+    // 128 -> 64 -> 32 with downsamples, 3x3 32 -> 16, visibility 128 -> 32)
+    const bool std_kh = p->kh_rb1.cin == 128 && p->kh_rb1.cout == 64 && p->kh_ds1.w && p->kh_rb2.cin == 64 &&
+                        p->kh_rb2.cout == 32 && p->kh_ds2.w && p->kh_c3.cin == 32 && p->kh_v1.cin == 128;
+    static const bool no_kh_split = getenv("KPD_NO_KH_SPLIT") != nullptr;   // A/B switch
+    if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty() && std_kh && !no_kh_split) {
+      chk(pack_split_kh(p, p->kh_s[0], 128, 128, 10, {{&p->kh_rb1, &p->kh_ds1, p->kh_bn1a_s, p->kh_bn1a_t, 0},
+                                                      {&p->kh_v1, nullptr, nullptr, nullptr, 64}}));
+      p->kh_s[0].ns = 64; p->kh_s[0].nf = 32;
+      chk(pack_split_kh(p, p->kh_s[1], 64, 64, 10, {{&p->kh_rb2, &p->kh_ds2, p->kh_bn1b_s, p->kh_bn1b_t, 0}}));
+      p->kh_s[1].ns = 32; p->kh_s[1].nf = 0;
+      chk(pack_split_kh(p, p->kh_s[2], 32, 64, 9, {{&p->kh_c3, nullptr, nullptr, nullptr, 0}}));
+      p->kh_s[2].ns = 0; p->kh_s[2].nf = 16;
+      p->kh_split = rc == KPD_OK;
+    }
   }
   if (!missing.empty()) return fail(KPD_ESTATE, "missing tensors: " + missing);
   if (rc != KPD_OK) return rc;
@@ -1145,10 +1255,45 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
 
 // KEYPOINT_HEAD (keypoint_head.py:50-62, ResidualBlock :64-90) on the
 // [R][56][56][128] NHWC ROI features in w.kx; outputs at the ROIs' slots.
-static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st) {
+// bound (split path): the bound of |x| for ROI r is bound[(r / bdiv) * bstride]
+static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st,
+                             const float* bound, int bdiv, int bstride) {
   const size_t px = (size_t)R * 3136;
   if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
     return rc;
+  if (p->kh_split && w.kxs) {
+    // fp32-accurate split products on zero-bordered maps (hmconv_kernel MODE 2):
+    // [ResidualBlock 1 (+ downsample as a tenth tap) | visibility conv] ->
+    // ResidualBlock 2 (+ downsample) -> regression 3x3; ReLU6 bounds every
+    // intermediate by 6, the input by the FPN level-0 maximum
+    HIP_TRY(launch_kh_att_split(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, R, bound, bdiv, bstride, w.hsc, w.kxs, st));
+    const void* ins[3] = {w.kxs, w.kr1s, w.kr2s};
+    void* outs[3] = {w.kr1s, w.kr2s, nullptr};
+    float* outf[3] = {w.kv1, nullptr, w.kr3};
+    for (int i = 0; i < 3; ++i) {
+      const KhSplit& k = p->kh_s[i];
+      HmConvArgs h{};
+      h.in = ins[i]; h.wt = k.ws; h.bias = k.b; h.out = outs[i]; h.outf = outf[i];
+      h.R = R; h.cin = k.cin; h.cout = k.cout; h.ntap = k.ntap; h.ns = k.ns; h.nf = k.nf;
+      h.kh_ps = k.ps; h.kh_pt = k.pt; h.kh_bd = k.ntap == 10 ? k.bd : nullptr;
+      h.split = 1; h.hsc = w.hsc; h.w_exp = k.w_exp;
+      h.in_c = i == 0 ? 0.f : 6.f; h.in_s = i == 0 ? 1.f : 0.f; h.in_idx = 2;
+      h.out_c = 6.f; h.out_s = 0.f; h.out_idx = k.ns > 0 ? 2 : -1; h.amax_idx = -1;
+      HIP_TRY(launch_hmconv(h, st));
+    }
+    const int o = p->kh_o, kr = pad16(16 * o * o);
+    if (kr != 16 * o * o) HIP_TRY(hipMemsetAsync(w.kpr, 0, sizeof(float) * R * kr, st));
+    HIP_TRY(launch_kh_pool(w.kr3, R, 16, o, w.kpr, kr, st));
+    HIP_TRY(launch_kh_pool(w.kv1, R, 32, 4, w.kpv, 512, st));
+    if (int rc = conv(p->kh_lr, w.kpr, R, 1, 1, kr, w.klr, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    if (int rc = conv(p->kh_lv, w.kpv, R, 1, 1, 512, w.klv, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+      return rc;
+    HIP_TRY(launch_kh_final(w.klr, p->kh_lr.cout_p, w.klv, p->kh_lv.cout_p, p->kh_lnr_g, p->kh_lnr_b, p->kh_fr_w,
+                            p->kh_fr_b, p->kh_lnv_g, p->kh_lnv_b, p->kh_fv_w, p->kh_fv_b, w.slot, R, P, kh_kpts,
+                            kh_vis, st));
+    return KPD_OK;
+  }
   HIP_TRY(launch_kh_att(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, px, st));
   // ResidualBlock(128 -> 64): relu6(relu6(bn1(relu6(conv_bn(x)))) + downsample(x))
   const float* id1 = w.kx;
@@ -1449,7 +1594,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   // given boxes for every image: the slot map rides along with the top-k launch
   const bool slot_in_topk = !detect && NB == B && NB * P > 0 && boxes != nullptr;
   HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st,
-                      slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr));
+                      slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr, w.imax));
   topk_stage.reset();
   if (int rc = mark(4)) return rc;
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
@@ -1501,7 +1646,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
     Stage sg(p, "keypoint_head", st);
     HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
-    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st)) return rc;
+    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1)) return rc;
   }
   return KPD_OK;
 }
@@ -1698,9 +1843,11 @@ int kpd_keypoint_head(kpd_plan* p, const float* x, int R, int H, int W, float* k
   HIP_TRY(hipSetDevice(p->device));
   Work* w = nullptr;
   if (int rc = op_work(p, R, KPD_FLAG_DUAL_HEAD, st, &w)) return rc;
-  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 128, 56, 56, w->kx, nullptr, st));
+  // any input sign: the split path's bound is max |x| per ROI (hsc[r][2])
+  if (p->kh_split) HIP_TRY(hipMemsetAsync(w->hsc, 0, sizeof(float) * 4 * R, st));
+  HIP_TRY(launch_nchw_rows_to_nhwc(x, R, 128, 56, 56, w->kx, nullptr, st, p->kh_split ? w->hsc + 2 : nullptr, 4));
   HIP_TRY(hipMemsetAsync(w->slot, 0, sizeof(int32_t) * R, st));
-  return run_keypoint_head(p, *w, R, 1, kpts, vis, st);
+  return run_keypoint_head(p, *w, R, 1, kpts, vis, st, w->hsc + 2, 1, 4);
 }
 
 int kpd_backbone(kpd_plan* p, const float* image, int B, int C, int H, int W, float* out0, float* out1, float* out2,
