@@ -13,6 +13,8 @@
 // on the MFMA conv kernel (post-affine epilogue for ResidualBlock.bn1),
 // adaptive pools (this file), the two Linear layers as MFMA GEMMs, and
 // LayerNorm + ReLU6 + Linear + sigmoid tails (this file).
+#include <algorithm>
+
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 
@@ -140,6 +142,108 @@ __global__ __launch_bounds__(256) void kh_att_split_kernel(const float* __restri
   }
 }
 
+// KEYPOINT_HEAD spatial attention fused (keypoint_head.py:15-20, 53-54):
+// att = sigmoid(b2 + w2 . relu6(W1 x + b1)) per pixel and xa = x * att written
+// as the split operand of the first KH hmconv (as kh_att_split_kernel).  A
+// workgroup takes 64 pixels of one ROI (3136 = 49 x 64; persistent over
+// tiles): x (fp32) stays in registers; x * 2^a as f16 hi / lo rows in LDS; the
+// 1x1 128 -> 64 on v_mfma_f32_16x16x32_f16 with three products (lo.hi, hi.hi,
+// hi.lo: fp32-accurate, the heatmap convs' split), wave w owning output
+// channels 16w .. 16w+15 with W1's fragments in registers for the whole launch;
+// the 64 -> 1 dot by 16-lane butterflies and a 4-wave LDS sum.  Replaces the
+// fp32 1x1 conv (whose [R][3136][64] output went through HBM) and one pass.
+constexpr int KA_ROW = 528;   // LDS bytes per pixel: hi 256 | lo 256 | 16 pad (b128 reads conflict-free)
+__global__ __launch_bounds__(256) void kh_att2_kernel(const float* __restrict__ x, const _Float16* __restrict__ w1s,
+                                                      int w1_exp, const float* __restrict__ b1,
+                                                      const float* __restrict__ w2, const float* __restrict__ b2,
+                                                      const float* __restrict__ bound, int bdiv, int bstride,
+                                                      float* __restrict__ hsc, int R, _Float16* __restrict__ out) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) char sx[64 * KA_ROW];
+  __shared__ float spart[4][64];
+  __shared__ float satt[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int co = wave * 16 + r16;
+  h8 bh[4], bl[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const _Float16* wp = w1s + (size_t)co * 256 + c * 64 + g * 8;
+    bh[c] = *reinterpret_cast<const h8*>(wp);
+    bl[c] = *reinterpret_cast<const h8*>(wp + 32);
+  }
+  const float bias1 = b1[co], wo2 = w2[co], bias2 = b2[0];
+  const int ntiles = R * 49, c4 = (tid & 31) * 4;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r = tile / 49, p0 = (tile - r * 49) * 64;
+    const float bnd = bound[(size_t)(r / bdiv) * bstride];
+    const int a = split_exp_of(bnd);
+    const float sc = ldexpf(1.f, a), us = ldexpf(1.f, -(a + w1_exp));
+    if (tid == 0 && p0 == 0) hsc[(size_t)r * 4 + 2] = bnd;
+    const float4* xp = reinterpret_cast<const float4*>(x + ((size_t)r * GP + p0) * 128);
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = xp[tid + 256 * i];   // pixel (tid >> 5) + 8 i, channels c4 .. c4 + 3
+    __syncthreads();   // the previous tile's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float e4[4] = {v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc};
+      f16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (_Float16)e4[e];
+        lo[e] = (_Float16)(e4[e] - (float)hi[e]);
+      }
+      char* rowp = sx + ((tid >> 5) + 8 * i) * KA_ROW + c4 * 2;
+      *reinterpret_cast<f16x4*>(rowp) = hi;
+      *reinterpret_cast<f16x4*>(rowp + 256) = lo;
+    }
+    __syncthreads();
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const char* rowp = sx + (i * 16 + r16) * KA_ROW + c * 64 + g * 16;
+        const h8 ah = *reinterpret_cast<const h8*>(rowp), al = *reinterpret_cast<const h8*>(rowp + 256);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[c], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[c], acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[c], acc[i], 0, 0, 0);
+      }
+    // lane (g, r16) holds pixels 16 i + 4 g + e of output channel co
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pv = wo2 * fminf(fmaxf(fmaf(acc[i][e], us, bias1), 0.f), 6.f);
+        pv += __shfl_xor(pv, 1);
+        pv += __shfl_xor(pv, 2);
+        pv += __shfl_xor(pv, 4);
+        pv += __shfl_xor(pv, 8);
+        if (r16 == 0) spart[wave][i * 16 + g * 4 + e] = pv;
+      }
+    __syncthreads();
+    if (tid < 64) satt[tid] = kpd_sigmoid(bias2 + ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid])));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int px = (tid >> 5) + 8 * i, pix = p0 + px, yy = pix / G, xx = pix - yy * G;
+      const float att = satt[px];
+      const float e4[4] = {(v[i].x * att) * sc, (v[i].y * att) * sc, (v[i].z * att) * sc, (v[i].w * att) * sc};
+      f16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hi[e] = (_Float16)e4[e];
+        lo[e] = (_Float16)(e4[e] - (float)hi[e]);
+      }
+      _Float16* o = out + (((size_t)r * (G + 2) + yy + 1) * (G + 2) + xx + 1) * 256 + (c4 / 32) * 64 + c4 % 32;
+      *reinterpret_cast<f16x4*>(o) = hi;
+      *reinterpret_cast<f16x4*>(o + 32) = lo;
+    }
+  }
+}
+
 // adaptive avg pool of an NHWC [R][56][56][C] map to (o x o), written in
 // NCHW-flatten order (c*o*o + y*o + x) as nn.Flatten after the pool does.
 // grid R, 256 threads over (c, y, x) outputs.
@@ -241,6 +345,25 @@ hipError_t launch_kh_att_split(const float* x, const float* sa1, const float* w,
   const size_t n = (size_t)R * GP;
   hipLaunchKernelGGL(kh_att_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, sa1, w, b, bound,
                      bdiv, bstride, hsc, R, static_cast<_Float16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_kh_att2(const float* x, const void* w1s, int w1_exp, const float* b1, const float* w2,
+                          const float* b2, int R, const float* bound, int bdiv, int bstride, float* hsc, void* out,
+                          hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  if (!w1s || !bound || bdiv < 1 || bstride < 1 || !hsc || !out) return hipErrorInvalidValue;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const long tiles = (long)R * 49;
+  const unsigned grid = (unsigned)std::min<long>(tiles, 4L * ncu);
+  hipLaunchKernelGGL(kh_att2_kernel, dim3(grid), dim3(256), 0, st, x, static_cast<const _Float16*>(w1s), w1_exp, b1,
+                     w2, b2, bound, bdiv, bstride, hsc, R, static_cast<_Float16*>(out));
   return hipGetLastError();
 }
 

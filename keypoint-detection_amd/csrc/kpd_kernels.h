@@ -292,6 +292,11 @@ hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float
 // the attention-weighted KEYPOINT_HEAD input as the split operand of the first
 // hmconv (KH mode): [R][58][58][128] f16 [hi32 | lo32], ROI r scaled by
 // 2^split_exp_of(bound[(r / bdiv) * bstride]), which is also stored to hsc[r][2]
+// the same with the spatial attention's 1x1 128 -> 64 fused (split f16 MFMA;
+// w1s = pack_split_1x1 layout [64][4][hi32 | lo32] scaled 2^w1_exp)
+hipError_t launch_kh_att2(const float* x, const void* w1s, int w1_exp, const float* b1, const float* w2,
+                          const float* b2, int R, const float* bound, int bdiv, int bstride, float* hsc, void* out,
+                          hipStream_t st);
 hipError_t launch_kh_att_split(const float* x, const float* sa1, const float* w, const float* b, int R,
                                const float* bound, int bdiv, int bstride, float* hsc, void* out, hipStream_t st);
 hipError_t launch_kh_pool(const float* in, int R, int C, int o, float* out, int out_stride, hipStream_t st);

@@ -296,6 +296,9 @@ int pack_conv(kpd_plan* p, const std::string& wname, const std::string& bias_nam
   const bool linear = w->shape.size() == 2 && k == 1;   // nn.Linear [out][in] as a 1x1 conv
   if (!linear && (w->shape.size() != 4 || w->shape[2] != k || w->shape[3] != k))
     return fail(KPD_EINVAL, "bad shape for " + wname);
+  dc.ws = nullptr;   // split copies belong to the previous finalize's (freed) allocations
+  dc.w_exp = 0;
+  dc.ws_kc = 0;
   dc.cout = (int)w->shape[0];
   dc.cin = (int)w->shape[1];
   dc.k = k;
@@ -1112,6 +1115,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
       p->kh_s[1].ns = 32; p->kh_s[1].nf = 0;
       chk(pack_split_kh(p, p->kh_s[2], 32, 64, 9, {{&p->kh_c3, nullptr, nullptr, nullptr, 0}}));
       p->kh_s[2].ns = 0; p->kh_s[2].nf = 16;
+      if (p->kh_sa1.cin_p == 128 && p->kh_sa1.cout_p == 64) chk(pack_split_1x1(p, p->kh_sa1));   // kh_att2_kernel
       p->kh_split = rc == KPD_OK;
     }
   }
@@ -1259,14 +1263,22 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
 static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st,
                              const float* bound, int bdiv, int bstride) {
   const size_t px = (size_t)R * 3136;
-  if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
-    return rc;
   if (p->kh_split && w.kxs) {
     // fp32-accurate split products on zero-bordered maps (hmconv_kernel MODE 2):
     // [ResidualBlock 1 (+ downsample as a tenth tap) | visibility conv] ->
     // ResidualBlock 2 (+ downsample) -> regression 3x3; ReLU6 bounds every
-    // intermediate by 6, the input by the FPN level-0 maximum
-    HIP_TRY(launch_kh_att_split(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, R, bound, bdiv, bstride, w.hsc, w.kxs, st));
+    // intermediate by 6, the input by the FPN level-0 maximum.  The spatial
+    // attention (1x1 convs + sigmoid + apply) is one kernel writing the first
+    // conv's operand (KPD_KH_ATT1=1: the fp32 1x1 conv + apply kernel, A/B).
+    static const bool att1 = getenv("KPD_KH_ATT1") != nullptr;
+    if (att1 || !p->kh_sa1.ws) {
+      if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+        return rc;
+      HIP_TRY(launch_kh_att_split(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, R, bound, bdiv, bstride, w.hsc, w.kxs, st));
+    } else {
+      HIP_TRY(launch_kh_att2(w.kx, p->kh_sa1.ws, p->kh_sa1.w_exp, p->kh_sa1.b, p->kh_sa2_w, p->kh_sa2_b, R, bound,
+                             bdiv, bstride, w.hsc, w.kxs, st));
+    }
     const void* ins[3] = {w.kxs, w.kr1s, w.kr2s};
     void* outs[3] = {w.kr1s, w.kr2s, nullptr};
     float* outf[3] = {w.kv1, nullptr, w.kr3};
@@ -1294,6 +1306,8 @@ static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts,
                             kh_vis, st));
     return KPD_OK;
   }
+  if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
+    return rc;
   HIP_TRY(launch_kh_att(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, px, st));
   // ResidualBlock(128 -> 64): relu6(relu6(bn1(relu6(conv_bn(x)))) + downsample(x))
   const float* id1 = w.kx;
