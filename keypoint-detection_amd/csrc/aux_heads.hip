@@ -246,18 +246,37 @@ __global__ __launch_bounds__(256) void kh_att2_kernel(const float* __restrict__ 
 
 // adaptive avg pool of an NHWC [R][56][56][C] map to (o x o), written in
 // NCHW-flatten order (c*o*o + y*o + x) as nn.Flatten after the pool does.
-// grid R, 256 threads over (c, y, x) outputs.
+// grid R, 256 threads.  Pass 1: item = (cell, source row, channel quad) sums
+// its row's columns with 16-byte loads (4 lanes read a pixel's 64 bytes)
+// into an LDS partial; pass 2: each output sums its cell's row partials in
+// row order.  LDS: o*o cells x rows-per-cell x C floats (host-sized).
 __global__ __launch_bounds__(256) void kh_pool_kernel(const float* __restrict__ in, int C, int o,
                                                       float* __restrict__ out, int out_stride) {
-  const int r = blockIdx.x;
+  extern __shared__ float part[];   // [cell][row in cell][C]
+  const int r = blockIdx.x, nq = C / 4, rpc = (G + o - 1) / o + 1;   // rows per cell (upper bound)
+  const float* src = in + (size_t)r * GP * C;
+  const int items = o * o * rpc * nq;
+  for (int t = threadIdx.x; t < items; t += blockDim.x) {
+    const int q = t % nq, rest = t / nq, dy = rest % rpc, cell = rest / rpc, i = cell / o, j = cell - i * o;
+    const int y0 = (i * G) / o, y1 = ((i + 1) * G + o - 1) / o;
+    const int x0 = (j * G) / o, x1 = ((j + 1) * G + o - 1) / o;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int y = y0 + dy;
+    if (y < y1)
+      for (int x = x0; x < x1; ++x) {
+        const float4 v = *reinterpret_cast<const float4*>(src + ((size_t)y * G + x) * C + q * 4);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    *reinterpret_cast<float4*>(part + ((size_t)cell * rpc + dy) * C + q * 4) = s;
+  }
+  __syncthreads();
   const int n = C * o * o;
   for (int t = threadIdx.x; t < n; t += blockDim.x) {
-    const int c = t / (o * o), rem = t - c * o * o, i = rem / o, j = rem - i * o;
+    const int c = t / (o * o), cell = t - c * o * o, i = cell / o, j = cell - i * o;
     const int y0 = (i * G) / o, y1 = ((i + 1) * G + o - 1) / o;
     const int x0 = (j * G) / o, x1 = ((j + 1) * G + o - 1) / o;
     float s = 0.f;
-    for (int y = y0; y < y1; ++y)
-      for (int x = x0; x < x1; ++x) s += in[(((size_t)r * G + y) * G + x) * C + c];
+    for (int dy = 0; dy < y1 - y0; ++dy) s += part[((size_t)cell * rpc + dy) * C + c];
     out[(size_t)r * out_stride + t] = s / (float)((y1 - y0) * (x1 - x0));
   }
 }
@@ -368,7 +387,10 @@ hipError_t launch_kh_att2(const float* x, const void* w1s, int w1_exp, const flo
 }
 
 hipError_t launch_kh_pool(const float* in, int R, int C, int o, float* out, int out_stride, hipStream_t st) {
-  hipLaunchKernelGGL(kh_pool_kernel, dim3(R), dim3(256), 0, st, in, C, o, out, out_stride);
+  if (C % 4 || o < 1 || o > G) return hipErrorInvalidValue;
+  const size_t lds = (size_t)o * o * ((G + o - 1) / o + 1) * C * sizeof(float);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kh_pool_kernel, dim3(R), dim3(256), lds, st, in, C, o, out, out_stride);
   return hipGetLastError();
 }
 

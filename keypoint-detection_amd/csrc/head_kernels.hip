@@ -160,7 +160,7 @@ __global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, in
 // Also emits per-(roi,row) channel sum/max partials for HeatmapHead attention.
 // CW = channels per lane: 1 -> the 64 top-k channels (HeatmapHead input),
 // 2 -> all 128 FPN channels in order (KEYPOINT_HEAD input, topk == nullptr).
-constexpr int kRoiStageFloats = 12800;   // 50 KB (4 rows x 50 columns of the 64 selected channels): 3 workgroups per CU
+constexpr int kRoiStageFloats = 12800;   // 50 KB (one interpolated row: 200 columns x 64 / 100 x 128 channels): 3 workgroups per CU
 template <int CW>
 __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
                                                         const int32_t* __restrict__ topk,
@@ -195,12 +195,16 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   for (int j = 0; j < NB; ++j)
 #pragma unroll
     for (int q = 0; q < CW; ++q) acc[j][q] = 0.f;
-  // Staged path (CW == 1): the output row's source pixels -- rows [ylo, yhi] x
-  // columns [xlo, xhi], every selected channel -- are gathered into LDS once
-  // (each element read from L2 once, instead of once per sample corner: ~4x
-  // fewer L2 bytes), then the samples read LDS.  Same sample positions,
-  // weights and summation order as the direct path; ROIs whose footprint
-  // exceeds the stage fall back to the direct gathers.
+  // Staged (separable) path: bilinear sampling is separable -- a sample's
+  // value is hx (hy F[yl][xl] + ly F[yh][xl]) + lx (hy F[yl][xh] + ly F[yh][xh])
+  // and the validity test is (y in range) && (x in range) -- so for each
+  // sample row iy the vertically interpolated row T[x] = hy F[yl][x] +
+  // ly F[yh][x] over the row's column span [xlo, xhi] is built in LDS once
+  // (each source element read from L2 once per sample row, not once per
+  // output bin and corner: ~3x fewer L1 / L2 loads), then every bin reads T at
+  // its two columns.  Same sample positions and weights as the direct path
+  // (the sums associate differently: fp32 rounding only).  Column spans wider
+  // than the stage fall back to the direct gathers.
   auto sample_y = [&](int iy, bool& yin, int& yl, int& yh, float& ly, float& hy) {
     const float y = y1 + (float)ph * bin_h + ((float)iy + 0.5f) * bin_h / (float)gh;
     yin = !(y < -1.f || y > (float)Hf);
@@ -220,52 +224,65 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     hx = 1.f - lx;
   };
   bool staged = false;
-  int ylo = 0, xlo = 0, nc = 0;
-  if constexpr (CW == 1) {
+  int xlo = 0, nc = 0;
+  {
     bool t0;
-    int a0, a1, yhi, xhi, d0;
+    int a0, xhi, d0;
     float f0, f1;
-    sample_y(0, t0, ylo, a1, f0, f1);
-    sample_y(gh - 1, t0, a0, yhi, f0, f1);
     sample_x(0, 0, xlo, d0, f0, f1, t0);
     sample_x(HM - 1, gw - 1, a0, xhi, f0, f1, t0);
-    const int nr = yhi - ylo + 1;
     nc = xhi - xlo + 1;
-    staged = nr > 0 && nc > 0 && nr * nc * CO <= stage_cap;   // stage_cap: the launch's dynamic LDS (floats)
-    if (staged) {
-      extern __shared__ float stage[];
-      const int chl = topk[b * TOPK + lane];
-      // a wave fills whole pixels: lane = channel (the top-k gather, 4 lines per instruction as before)
-      for (int px = wave; px < nr * nc; px += 4) {
-        const int ry = px / nc, cx2 = px - ry * nc;
-        stage[px * CO + lane] = fb[((size_t)(ylo + ry) * Wf + xlo + cx2) * Cf + chl];
+    staged = nc > 0 && nc * CO <= stage_cap;   // stage_cap: the launch's dynamic LDS (floats)
+  }
+  if (staged) {
+    extern __shared__ float stage[];
+    int chs[CW];
+#pragma unroll
+    for (int q = 0; q < CW; ++q) chs[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
+    for (int iy = 0; iy < gh; ++iy) {
+      bool yin;
+      int yl, yh;
+      float ly, hy;
+      sample_y(iy, yin, yl, yh, ly, hy);
+      if (iy) __syncthreads();   // every bin finished reading the previous row's T
+      const float* r1 = fb + (size_t)yl * Wf * Cf;
+      const float* r2 = fb + (size_t)yh * Wf * Cf;
+      // 8 columns per wave per batch, every load of a batch in flight before
+      // the first use (one L2 round trip per batch instead of per column)
+      constexpr int UB = 8;
+      for (int base = wave; base < nc; base += 4 * UB) {
+        float v1[UB][CW], v2[UB][CW];
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int px = min(base + 4 * u, nc - 1);
+          const size_t o = (size_t)(xlo + px) * Cf;
+#pragma unroll
+          for (int q = 0; q < CW; ++q) {
+            v1[u][q] = r1[o + chs[q]];
+            v2[u][q] = r2[o + chs[q]];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int px = base + 4 * u;
+          if (px < nc)
+#pragma unroll
+            for (int q = 0; q < CW; ++q) stage[px * CO + lane + TOPK * q] = yin ? hy * v1[u][q] + ly * v2[u][q] : 0.f;
+        }
       }
       __syncthreads();
-      for (int iy = 0; iy < gh; ++iy) {
-        bool yin;
-        int yl, yh;
-        float ly, hy;
-        sample_y(iy, yin, yl, yh, ly, hy);
-        const int r1 = (yl - ylo) * nc, r2 = (yh - ylo) * nc;
-        for (int ix = 0; ix < gw; ++ix) {
-          float v[NB][4], wgt[NB][4];
+      for (int ix = 0; ix < gw; ++ix) {
 #pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            int xl, xh;
-            float lx, hx;
-            bool xin;
-            sample_x(wave + 4 * j, ix, xl, xh, lx, hx, xin);
-            const bool in = yin && xin;
-            wgt[j][0] = in ? hy * hx : 0.f; wgt[j][1] = in ? hy * lx : 0.f;
-            wgt[j][2] = in ? ly * hx : 0.f; wgt[j][3] = in ? ly * lx : 0.f;
-            v[j][0] = stage[(r1 + xl - xlo) * CO + lane];
-            v[j][1] = stage[(r1 + xh - xlo) * CO + lane];
-            v[j][2] = stage[(r2 + xl - xlo) * CO + lane];
-            v[j][3] = stage[(r2 + xh - xlo) * CO + lane];
+        for (int j = 0; j < NB; ++j) {
+          int xl, xh;
+          float lx, hx;
+          bool xin;
+          sample_x(wave + 4 * j, ix, xl, xh, lx, hx, xin);
+#pragma unroll
+          for (int q = 0; q < CW; ++q) {
+            const float v = hx * stage[(xl - xlo) * CO + lane + TOPK * q] + lx * stage[(xh - xlo) * CO + lane + TOPK * q];
+            acc[j][q] += xin ? v : 0.f;
           }
-#pragma unroll
-          for (int j = 0; j < NB; ++j)
-            acc[j][0] += wgt[j][0] * v[j][0] + wgt[j][1] * v[j][1] + wgt[j][2] * v[j][2] + wgt[j][3] * v[j][3];
         }
       }
     }
@@ -638,8 +655,10 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
                        roi, roi_stats, cap);
   } else {
     if (Cf != 2 * TOPK) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), 0, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
-                       roi, nullptr, 0);
+    static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
+    const int cap = direct ? 0 : kRoiStageFloats;
+    hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
+                       roi, nullptr, cap);
   }
   return hipGetLastError();
 }
