@@ -250,6 +250,19 @@ int kpd_roi_align(const float* features, int B, int C, int H, int W, const float
 int kpd_conv1x1(const float* x, int B, int Cin, int HW, const float* w, const float* b, int Cout, float* out,
                 void* stream);
 
+/* Training side (the backward of the heatmap head's 3x3
+ * convolutions: nn.Conv2d(C, O, 3, padding=1), heatmap_head.py:31-45,55-66,
+ * whose gradients the reference takes from autograd in Trainer.train,
+ * trainer.py:263,272).  NCHW fp32 device tensors, exact fp32 products
+ * (v_mfma_f32_16x16x4_f32), deterministic fixed-order sums.
+ *   kpd_conv3x3_forward:  y [N][O][H][W] = conv(x [N][C][H][W], w [O][C][3][3]) + b (b nullable)
+ *   kpd_conv3x3_backward: for gy = dL/dy [N][O][H][W]: gx = dL/dx, gw = dL/dw
+ *                         [O][C][3][3], gb = dL/db [O] (each nullable). */
+int kpd_conv3x3_forward(const float* x, const float* w, const float* b, int N, int C, int H, int W, int O, float* y,
+                        void* stream);
+int kpd_conv3x3_backward(const float* x, const float* w, const float* gy, int N, int C, int H, int W, int O,
+                         float* gx, float* gw, float* gb, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -324,3 +324,10 @@ hipError_t launch_gather_planes(const float* x, int N, int C, int HW, const int3
 hipError_t launch_conv1x1_nchw(const float* x, int N, int Cin, int HW, const float* w, const float* b, int Cout,
                                float* out, hipStream_t st);
 hipError_t launch_fill(float* p, long n, float v, hipStream_t st);
+
+// ---- the heatmap head's 3x3 conv forward / backward on NCHW (conv3_grad.hip) ----
+hipError_t launch_conv3_forward(const float* x, const float* w, const float* b, int N, int C, int H, int W, int O,
+                                float* y, hipStream_t st);
+size_t conv3_wgrad_slices(int N, int H, int W);   // wgrad_part: slices * O * 9C floats
+hipError_t launch_conv3_backward(const float* x, const float* w, const float* gy, int N, int C, int H, int W, int O,
+                                 float* gx, float* gw, float* gb, float* wgrad_part, hipStream_t st);

@@ -1957,6 +1957,37 @@ int kpd_conv1x1(const float* x, int B, int Cin, int HW, const float* w, const fl
   return KPD_OK;
 }
 
+int kpd_conv3x3_forward(const float* x, const float* w, const float* b, int N, int C, int H, int W, int O, float* y,
+                        void* stream) {
+  if (N < 0 || C <= 0 || H <= 0 || W <= 0 || O <= 0 || (N > 0 && (!x || !w || !y)))
+    return fail(KPD_EINVAL, "bad conv3x3 arguments");
+  if ((long)N * C * H * W >= (1L << 31) || (long)N * O * H * W >= (1L << 31) || (long)O * C * 9 >= (1L << 31))
+    return fail(KPD_EINVAL, "conv3x3: tensors must stay below 2^31 elements");
+  HIP_TRY(launch_conv3_forward(x, w, b, N, C, H, W, O, y, reinterpret_cast<hipStream_t>(stream)));
+  return KPD_OK;
+}
+
+int kpd_conv3x3_backward(const float* x, const float* w, const float* gy, int N, int C, int H, int W, int O,
+                         float* gx, float* gw, float* gb, void* stream) {
+  if (N < 0 || C <= 0 || H <= 0 || W <= 0 || O <= 0 || (N > 0 && !gy) || (gx && !w) || (gw && !x))
+    return fail(KPD_EINVAL, "bad conv3x3 backward arguments");
+  if ((long)N * C * H * W >= (1L << 31) || (long)N * O * H * W >= (1L << 31) || (long)O * C * 9 >= (1L << 31))
+    return fail(KPD_EINVAL, "conv3x3: tensors must stay below 2^31 elements");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (N == 0) {   // empty batch: zero parameter gradients
+    if (gw) HIP_TRY(hipMemsetAsync(gw, 0, sizeof(float) * O * C * 9, st));
+    if (gb) HIP_TRY(hipMemsetAsync(gb, 0, sizeof(float) * O, st));
+    return KPD_OK;
+  }
+  float* part = nullptr;
+  if (gw) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&part),
+                                 sizeof(float) * conv3_wgrad_slices(N, H, W) * O * C * 9, st));
+  const hipError_t e = launch_conv3_backward(x, w, gy, N, C, H, W, O, gx, gw, gb, part, st);
+  if (part) HIP_TRY(hipFreeAsync(part, st));
+  HIP_TRY(e);
+  return KPD_OK;
+}
+
 int kpd_nms(const float* boxes, const float* scores, int n, float thr, int max_out, int32_t* keep, int32_t* n_keep,
             void* stream) {
   if (n < 0 || (n > 0 && (!boxes || !scores || !keep)) || !n_keep) return fail(KPD_EINVAL, "bad nms args");

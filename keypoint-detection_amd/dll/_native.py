@@ -31,7 +31,8 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_bench_conv16",
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
            "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
-           "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss")
+           "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss", "kpd_conv3x3_forward",
+           "kpd_conv3x3_backward")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 HEAD_CHANNEL_ATT, HEAD_SPATIAL_ATT, HEAD_CONVS, HEAD_ALL = 1, 2, 4, 7
@@ -93,6 +94,10 @@ def load() -> ctypes.CDLL:
     lib.kpd_conv1x1.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
     lib.kpd_adaptive_heatmap_loss.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
                                               c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kpd_conv3x3_forward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                        c_void_p]
+    lib.kpd_conv3x3_backward.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]
     for name in EXPORTS:
         if name not in ("kpd_last_error", "kpd_version", "kpd_plan_destroy"):
             getattr(lib, name).restype = c_int
@@ -299,6 +304,43 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor])
         check(lib.kpd_conv1x1(_ptr(x), B, C, H * W, _ptr(w), _ptr(b), w.shape[0], _ptr(out), _stream(x.device)),
               "kpd_conv1x1")
     return out
+
+
+def conv3x3_forward(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """nn.Conv2d(k=3, padding=1) forward on NCHW device tensors (kpd_conv3x3_forward)."""
+    x = _dev_f32(x, "x")
+    N, C, H, W = x.shape
+    w = weight.detach().to(x.device, torch.float32).contiguous()
+    if w.dim() != 4 or w.shape[1] != C or w.shape[2:] != (3, 3):
+        raise ValueError(f"weight must be [O][{C}][3][3], got {tuple(w.shape)}")
+    b = None if bias is None else bias.detach().to(x.device, torch.float32).contiguous()
+    y = torch.empty(N, w.shape[0], H, W, device=x.device)
+    lib = load()
+    with torch.cuda.device(x.device):
+        check(lib.kpd_conv3x3_forward(_ptr(x), _ptr(w), _ptr(b), N, C, H, W, w.shape[0], _ptr(y), _stream(x.device)),
+              "kpd_conv3x3_forward")
+    return y
+
+
+def conv3x3_backward(x: torch.Tensor, weight: torch.Tensor, grad_y: torch.Tensor, need_x: bool = True,
+                     need_w: bool = True, need_b: bool = True):
+    """Gradients of nn.Conv2d(k=3, padding=1) (kpd_conv3x3_backward): (gx, gw, gb),
+    None where not requested."""
+    x = _dev_f32(x, "x")
+    N, C, H, W = x.shape
+    w = weight.detach().to(x.device, torch.float32).contiguous()
+    O = w.shape[0]
+    gy = _dev_f32(grad_y, "grad_y")
+    if tuple(gy.shape) != (N, O, H, W):
+        raise ValueError(f"grad_y must be [{N}][{O}][{H}][{W}], got {tuple(gy.shape)}")
+    gx = torch.empty_like(x) if need_x else None
+    gw = torch.empty_like(w) if need_w else None
+    gb = torch.empty(O, device=x.device) if need_b else None
+    lib = load()
+    with torch.cuda.device(x.device):
+        check(lib.kpd_conv3x3_backward(_ptr(x), _ptr(w), _ptr(gy), N, C, H, W, O, _ptr(gx), _ptr(gw), _ptr(gb),
+                                       _stream(x.device)), "kpd_conv3x3_backward")
+    return gx, gw, gb
 
 
 class PlanCache:
