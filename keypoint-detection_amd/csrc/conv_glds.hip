@@ -1443,7 +1443,10 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
     // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
     // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
     float* tile = reinterpret_cast<float*>(lds);
-    constexpr int P4 = 128 + 4, C4 = 32, RS = NTH / C4, IT = BMH / RS;
+    // a thread takes 8 consecutive channels of a row: 16-byte stores (the
+    // epilogue's store tail is issue-bound when every CU stores at once:
+    // half the store instructions of 8-byte pieces)
+    constexpr int P4 = 128 + 4, C8 = 16, RS = NTH / C8, IT = (BMH + RS - 1) / RS;
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
     float mx[2] = {0.f, 0.f};   // SPLIT: max|out| of the tile's two ROIs (>= 0 after ReLU)
 #pragma unroll
@@ -1451,36 +1454,40 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
       if (h) __syncthreads();
       if (wn / 2 == h) acc_to_lds<FM, FN, WM, 64, 128>(tile, acc, wm, wn % 2, lane);
       __syncthreads();
-      const int c4 = tid % C4, row0 = tid / C4, co = n0 + h * 128 + c4 * 4;
-      const float4 b = *reinterpret_cast<const float4*>(p.bias + co);
+      const int c8 = tid % C8, row0 = tid / C8, co = n0 + h * 128 + c8 * 8;
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + co);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + co + 4);
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int row = row0 + it * RS, m = m0 + row;
         int r, yy, xx;
-        if (!interior(m, r, yy, xx)) continue;
-        float4 x = *reinterpret_cast<const float4*>(tile + row * P4 + c4 * 4);
+        if (row >= BMH || !interior(m, r, yy, xx)) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8 + 4);
+        float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         if constexpr (SPLIT) {
           const int q = m >= rbound;
           const float u = q ? us[1] : us[0], sc = q ? os[1] : os[0];
-          x.x = fmaxf(fmaf(x.x, u, b.x), 0.f); x.y = fmaxf(fmaf(x.y, u, b.y), 0.f);
-          x.z = fmaxf(fmaf(x.z, u, b.z), 0.f); x.w = fmaxf(fmaf(x.w, u, b.w), 0.f);
-          const float xv[4] = {x.x, x.y, x.z, x.w};
-          f16x4 hi, lo;
+          f16x8 hi, lo;
+          float mc = 0.f;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int e = 0; e < 8; ++e) {
+            xv[e] = fmaxf(fmaf(xv[e], u, bv[e]), 0.f);
+            mc = fmaxf(mc, xv[e]);
             const float xs = xv[e] * sc;
             hi[e] = (_Float16)xs;
             lo[e] = (_Float16)(xs - (float)hi[e]);
           }
           char* ob = static_cast<char*>(p.out) + (size_t)m * (p.cout * 4) + (co >> 5) * 128 + (co & 31) * 2;
-          *reinterpret_cast<f16x4*>(ob) = hi;
-          *reinterpret_cast<f16x4*>(ob + 64) = lo;
-          const float mc = fmaxf(fmaxf(x.x, x.y), fmaxf(x.z, x.w));
+          *reinterpret_cast<f16x8*>(ob) = hi;
+          *reinterpret_cast<f16x8*>(ob + 64) = lo;
           if (q) mx[1] = fmaxf(mx[1], mc); else mx[0] = fmaxf(mx[0], mc);
         } else {
-          x.x = fmaxf(x.x + b.x, 0.f); x.y = fmaxf(x.y + b.y, 0.f);
-          x.z = fmaxf(x.z + b.z, 0.f); x.w = fmaxf(x.w + b.w, 0.f);
-          store4<__bf16>(out + (size_t)m * p.cout + co, x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xv[e] = fmaxf(xv[e] + bv[e], 0.f);
+          store4<__bf16>(out + (size_t)m * p.cout + co, make_float4(xv[0], xv[1], xv[2], xv[3]));
+          store4<__bf16>(out + (size_t)m * p.cout + co + 4, make_float4(xv[4], xv[5], xv[6], xv[7]));
         }
       }
     }
