@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
                                                    const float* __restrict__ w2, const float* __restrict__ b2,
                                                    int32_t* __restrict__ topk, float* __restrict__ scores_out,
                                                    const float* __restrict__ boxes, int P, int32_t* __restrict__ slot,
-                                                   float* __restrict__ imax) {
+                                                   float* __restrict__ imax, float* __restrict__ sc_zero, int sc_n) {
   extern __shared__ __attribute__((aligned(16))) float tsm[];
   // more tiles than fit in LDS (the fp32 path's small tiles at 384x288):
   // the partials are summed straight from global memory
@@ -100,6 +100,13 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
     // (optional) the image's max over FPN level 0 (its channel maxima; the map
     // follows a ReLU, so this is max |x|): the bound of the KEYPOINT_HEAD's
     // split operand, whose ROI features interpolate this map
+    // (optional) zero the image's split-scale slots (max |tap0|, max |lateral 1|,
+    // atomicMax targets of the stem and lateral-1 conv): FPN level 0 has read
+    // them, and the next forward's producers need them zero (no memset launch)
+    if (sc_zero && c == 129) {
+      sc_zero[(size_t)n * kAmaxStride] = 0.f;
+      sc_zero[(size_t)(sc_n + n) * kAmaxStride] = 0.f;
+    }
     if (imax && c == 128) {
       float M = 0.f;
       for (int k = 0; k < FC; ++k) M = fmaxf(M, mx[k]);
@@ -634,11 +641,11 @@ __global__ __launch_bounds__(64) void decode_kernel(const float* __restrict__ he
 
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
-                       const float* boxes, int P, int32_t* slot, float* imax) {
+                       const float* boxes, int P, int32_t* slot, float* imax, float* sc_zero, int sc_n) {
   if (slot && (!boxes || P <= 0 || P > 0xFFFF)) return hipErrorInvalidValue;
   const size_t lds = ((size_t)(tiles <= kTopkMaxTiles ? tiles : 0) * 2 * FC + 2 * 8 * FC) * 4;
   hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores,
-                     boxes, P, slot, imax);
+                     boxes, P, slot, imax, sc_zero, sc_n);
   return hipGetLastError();
 }
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipStream_t st) {

@@ -250,7 +250,8 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
 // slot != nullptr: also writes the slot map of boxes [N][P][4] (launch_slotmap's work)
 hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float* w0, const float* b0,
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
-                       const float* boxes = nullptr, int P = 0, int32_t* slot = nullptr, float* imax = nullptr);
+                       const float* boxes = nullptr, int P = 0, int32_t* slot = nullptr, float* imax = nullptr,
+                       float* sc_zero = nullptr, int sc_n = 0);
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,

@@ -141,6 +141,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   long cbd_floats = 0;
   float* separt = nullptr;  // [B][kSePartFloats] SE fc1 partials (exdw_kernel -> seproj_kernel)
   float* sc = nullptr;    // split FPN scale inputs: per-image max|tap0| [B], max|lateral1| [B] (amax_publish_img)
+  bool sc_dirty = true;   // sc may hold a previous forward's maxima (topk_kernel re-zeroes it)
   // person-detector glue
   float* pd_pool = nullptr;     // [B][56*56][128]
   float* pd_head = nullptr;     // [B][56*56][48]
@@ -1162,6 +1163,7 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
     p->ws_bytes[k] = need;
   }
   carve(p, d, reinterpret_cast<char*>(p->ws[k]), p->work[k]);
+  p->work[k].sc_dirty = true;
   // zero once: the padded heatmap-conv maps keep their zero border (the
   // kernels write interiors only)
   if (hm_padded(p)) HIP_TRY(hipMemsetAsync(p->ws[k], 0, need, st));
@@ -1407,7 +1409,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
 
   // ---------------- MobileNetV3-Small body ----------------
   std::unique_ptr<Stage> body_stage(new Stage(p, "body", st));
-  if (lin) HIP_TRY(hipMemsetAsync(w.sc, 0, (size_t)2 * B * kAmaxStride * sizeof(float), st));
+  if (lin && w.sc_dirty) HIP_TRY(hipMemsetAsync(w.sc, 0, (size_t)2 * B * kAmaxStride * sizeof(float), st));
+  if (lin) w.sc_dirty = true;   // until this forward's topk_kernel zeroes the slots it used
   HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], lin ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
@@ -1608,7 +1611,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   // given boxes for every image: the slot map rides along with the top-k launch
   const bool slot_in_topk = !detect && NB == B && NB * P > 0 && boxes != nullptr;
   HIP_TRY(launch_topk(w.stats, B, d.tiles, HWf, p->ca_w0, p->ca_b0, p->ca_w2, p->ca_b2, w.topk, w.scores, st,
-                      slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr, w.imax));
+                      slot_in_topk ? boxes : nullptr, P, slot_in_topk ? w.slot : nullptr, w.imax,
+                      lin ? w.sc : nullptr, B));
+  if (lin) w.sc_dirty = false;
   topk_stage.reset();
   if (int rc = mark(4)) return rc;
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
