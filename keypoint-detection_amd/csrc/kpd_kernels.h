@@ -243,6 +243,22 @@ hipError_t launch_pw_small(const ConvArgs& a, hipStream_t st);
 hipError_t launch_se_excite(const SeProjArgs& a, int N, float* sesc, hipStream_t st);
 hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles, float* stats,
                                 hipStream_t st);
+// LightweightFPN laterals 3 -> 2 -> 1 with the top-down adds in one launch
+// (lateral_chain.hip): taps t_i NHWC [N][h_i * w_i][c_i] (c_i = padded input
+// channels: 32, 48, 576; lateral 3 at most 128 pixels), weights L_i
+// [128][c_i] (no bias); writes lat1 [N][h1*w1][128]
+// and (amax != null) per-image max |lat1| at amax[n * kAmaxStride]
+struct LatChainArgs {
+  const float *t1, *t2, *t3, *L1, *L2, *L3;
+  int c1, c2, c3, h1, w1, h2, w2, h3, w3;
+  int n;   // images (set by launch_lateral_chain)
+  float* lat1;
+  float* amax;
+  unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
+};
+size_t lateral_chain_lds_bytes(const LatChainArgs& a);
+bool lateral_chain_ok(const LatChainArgs& a);   // shapes launch_lateral_chain takes
+hipError_t launch_lateral_chain(const LatChainArgs& a, int N, hipStream_t st);
 hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, const float* bias, const float* res,
                                  int N, int H, int W, int rh, int rw, void* out, hipStream_t st);
 

@@ -234,6 +234,7 @@ struct kpd_plan {
   // pipelined sub-batches (KPD_PIPE): sub-batch k+1 starts when sub-batch k
   // passes a stage mark, so its latency-bound body overlaps k's heavy stages
   hipEvent_t pipe_ev[kMaxSub] = {};
+  bool keep_laterals = false;   // kpd_backbone: every lateral level is an output (no fused chain)
   hipStream_t sub_st_pri[kMaxSub] = {};   // high-priority sub-batch streams (KPD_PIPE_PRI)
   std::map<std::string, std::pair<const void*, size_t>> debug;
   unsigned long long* stamps = nullptr;   // KPD_STAMPS diagnostic buffer (kStampWords)
@@ -1556,7 +1557,25 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
   const int lh[4] = {d.h[0], d.h[3], d.h[8], d.h[11]}, lw[4] = {d.w[0], d.w[3], d.w[8], d.w[11]};
   std::unique_ptr<Stage> lat_stage(new Stage(p, "fpn_lateral", st));
+  // laterals 3 -> 1 in one launch (lateral_chain.hip) when only lateral 1 is
+  // consumed (kpd_backbone returns every level: the per-level convs then)
+  static const bool no_chain = getenv("KPD_NO_LAT_CHAIN") != nullptr;   // A/B switch
+  LatChainArgs lc{};
+  lc.t1 = taps[1]; lc.t2 = taps[2]; lc.t3 = taps[3];
+  lc.L1 = static_cast<const float*>(p->lat[1].w); lc.L2 = static_cast<const float*>(p->lat[2].w);
+  lc.L3 = static_cast<const float*>(p->lat[3].w);
+  lc.c1 = pad16(kFpnIn[1]); lc.c2 = pad16(kFpnIn[2]); lc.c3 = pad16(kFpnIn[3]);
+  lc.h1 = lh[1]; lc.w1 = lw[1]; lc.h2 = lh[2]; lc.w2 = lw[2]; lc.h3 = lh[3]; lc.w3 = lw[3];
+  lc.lat1 = w.lat[1];
+  lc.amax = lin ? w.sc + (size_t)B * kAmaxStride : nullptr;
+  lc.stamps = take_stamps("stamps_latchain_0", (size_t)8 * ((B + 7) / 8 * 8));
+  const bool chain = !no_chain && !p->keep_laterals && !p->lat[1].bf16 && !p->lat[2].bf16 && !p->lat[3].bf16 &&
+                     p->lat[1].cin_p == lc.c1 && p->lat[2].cin_p == lc.c2 && p->lat[3].cin_p == lc.c3 &&
+                     p->lat[1].cout_p == 128 && p->lat[2].cout_p == 128 && p->lat[3].cout_p == 128 &&
+                     lateral_chain_ok(lc);
+  if (chain) HIP_TRY(launch_lateral_chain(lc, B, st));
   for (int i = 3; i >= 0; --i) {
+    if (chain && i > 0) continue;
     const DevConv& L = p->lat[i];
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
     if (i == 0 && lin) {   // no lateral 0: tap0 and lateral 1 go to the split layouts fpn0x_kernel reads
@@ -1894,9 +1913,11 @@ int kpd_backbone(kpd_plan* p, const float* image, int B, int C, int H, int W, fl
   const int cap = max_pass_images(H, W), npass = (B + cap - 1) / cap;
   for (int q = 0; q < npass; ++q) {
     const int b0 = (int)((long)B * q / npass), b1 = (int)((long)B * (q + 1) / npass), nb = b1 - b0;
-    if (int rc = forward_one(p, 0, false, image + (size_t)b0 * C * H * W, nb, C, H, W, nullptr, 0, 0, 0, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st))
-      return rc;
+    p->keep_laterals = true;
+    const int rc1 = forward_one(p, 0, false, image + (size_t)b0 * C * H * W, nb, C, H, W, nullptr, 0, 0, 0, nullptr,
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st);
+    p->keep_laterals = false;
+    if (rc1) return rc1;
     Work& w = p->work[0];
     HIP_TRY(launch_nhwc_to_nchw(w.feat, nb, lh[0] * lw[0], 128, outs[0] + (size_t)b0 * 128 * lh[0] * lw[0], st));
     for (int i = 1; i < 4; ++i) {   // fpn_convs[i] on lateral i (backbone.py:39), into the free level-0 buffer

@@ -1,0 +1,213 @@
+// LightweightFPN laterals as one launch (reference dll/models/backbone.py:
+// 29-39): lat3 = L3 . tap3, lat2 = L2 . tap2 + up(lat3), lat1 = L1 . tap1 +
+// up(lat2) (1x1 convs without bias, nearest top-down upsampling as
+// F.interpolate(size=...)).  The top-down adds are channel-wise, so a
+// workgroup takes one image and 16 output channels and runs the whole chain
+// with lat3 / lat2 in LDS: only lat1 reaches HBM (the split-mode FPN level 0
+// reads lat1 and the stem tap; lateral 0 is never materialised).  Replaces
+// five launches (lateral 3 split-K GEMM + reduce, lateral 2, lateral 1) whose
+// cost was latency, not work.  gfx950:
+//   * 1x1 convs on v_mfma_f32_16x16x4_f32 (exact fp32 products; a lane's
+//     float4 of 4 consecutive input channels feeds 4 MFMAs, with the weights
+//     permuted alike), operands straight from L2;
+//   * lat3 (few pixels, K = 576) splits K over the 4 waves, partial sums added
+//     in wave order; lat2 / lat1 split the pixel tiles over the waves;
+//   * per-image max |lat1| published for the split FPN scale (as the generic
+//     conv epilogue did).
+#include <algorithm>
+
+#include "kpd_common.h"
+#include "kpd_kernels.h"
+
+namespace {
+
+constexpr int LG = 16;   // output channels per workgroup
+
+__device__ __forceinline__ int up_index(int y, int H, int h) {   // nearest, F.interpolate(size=(H, .)) from h
+  return H == h ? y : min((int)floorf((float)y * ((float)h / (float)H)), h - 1);
+}
+
+// diagnostic phase stamps (KPD_STAMPS): thread 0, s_memrealtime, row [8] per workgroup
+__device__ __forceinline__ void stamp(unsigned long long* st, int i) {
+  if (st && threadIdx.x == 0)
+    st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
+// MFMA over one 16-channel K chunk: lane (g, r16) supplies A[px r16][4g .. 4g+3]
+// and B[co r16][4g .. 4g+3]
+__device__ __forceinline__ f32x4 mfma_k16(const float4 a, const float4 b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+}
+
+// NK1 / NK2 / NK3: 16-channel K chunks of laterals 1 / 2 / 3 (the model's 24
+// -> 32, 48 and 576 input channels); T3: lateral-3 tiles (at most 16 * T3
+// pixels).  Eight waves; every phase issues all its independent loads before
+// its MFMAs, so a phase costs about one memory round trip: the chain is
+// latency, not bandwidth (a 256x192 image's whole chain reads 0.3 MB).
+constexpr int NW = 8;
+
+template <int NK1, int NK2, int NK3, int T3>
+__global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float lsm[];
+  const int P1 = p.h1 * p.w1, P2 = p.h2 * p.w2, P3 = p.h3 * p.w3;
+  float* l3 = lsm;                      // [P3][16]
+  float* l2 = l3 + P3 * LG;             // [P2][16]
+  float* red = l2;                      // [NW][P3][16] lat3 partials (dead before l2 is written)
+  // grid (B rounded up to 8, 8): workgroup id b + Bp * cg sits on XCD b % 8,
+  // so an image's 8 channel groups share one L2 and its taps leave HBM once
+  const int b = blockIdx.x, cg = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (b >= p.n) return;
+  const int g = lane >> 4, r16 = lane & 15, co = cg * LG + r16;
+  const float* t1 = p.t1 + (size_t)b * P1 * (NK1 * 16) + 4 * g;
+  const float* t2 = p.t2 + (size_t)b * P2 * (NK2 * 16) + 4 * g;
+  const float* t3 = p.t3 + (size_t)b * P3 * (NK3 * 16) + 4 * g;
+  stamp(p.stamps, 0);
+
+  // lat3: every tile at once, K chunks q = wave + NW * u (partials added in wave order)
+  {
+    constexpr int U3 = (NK3 + NW - 1) / NW;
+    const int nt3 = (P3 + 15) / 16;
+    const float* brow = p.L3 + (size_t)co * (NK3 * 16) + 4 * g;
+    float4 bb[U3], a[U3][T3];
+#pragma unroll
+    for (int u = 0; u < U3; ++u) {
+      const int q = min(wave + NW * u, NK3 - 1);
+      bb[u] = *reinterpret_cast<const float4*>(brow + q * 16);
+#pragma unroll
+      for (int t = 0; t < T3; ++t)
+        a[u][t] = *reinterpret_cast<const float4*>(t3 + (size_t)min(t * 16 + r16, P3 - 1) * (NK3 * 16) + q * 16);
+    }
+    f32x4 acc[T3];
+#pragma unroll
+    for (int t = 0; t < T3; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U3; ++u)
+      if (wave + NW * u < NK3)
+#pragma unroll
+        for (int t = 0; t < T3; ++t) acc[t] = mfma_k16(a[u][t], bb[u], acc[t]);
+#pragma unroll
+    for (int t = 0; t < T3; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int pp = t * 16 + 4 * g + e;
+        if (t < nt3 && pp < P3) red[(wave * P3 + pp) * LG + r16] = acc[t][e];
+      }
+  }
+  stamp(p.stamps, 1);
+  __syncthreads();
+  for (int i = tid; i < P3 * LG; i += NW * 64) {
+    float v = red[i];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w * P3 * LG + i];
+    l3[i] = v;
+  }
+  __syncthreads();
+  stamp(p.stamps, 2);
+
+  // lat2 = L2 . tap2 + up(lat3): wave takes tiles wave + NW * j in batches of JB
+  {
+    constexpr int JB = 2;
+    float4 bw[NK2];
+#pragma unroll
+    for (int k = 0; k < NK2; ++k) bw[k] = *reinterpret_cast<const float4*>(p.L2 + (size_t)co * (NK2 * 16) + 4 * g + 16 * k);
+    const int nt2 = (P2 + 15) / 16;
+    for (int t0 = wave; t0 < nt2; t0 += NW * JB) {
+      float4 a[JB][NK2];
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const int px = min((t0 + NW * j) * 16 + r16, P2 - 1);
+#pragma unroll
+        for (int k = 0; k < NK2; ++k) a[j][k] = *reinterpret_cast<const float4*>(t2 + (size_t)px * (NK2 * 16) + 16 * k);
+      }
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const int t = t0 + NW * j;
+        if (t >= nt2) break;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < NK2; ++k) acc = mfma_k16(a[j][k], bw[k], acc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int pp = t * 16 + 4 * g + e;
+          if (pp >= P2) continue;
+          const int y = pp / p.w2, x = pp - y * p.w2;
+          const int sy = up_index(y, p.h2, p.h3), sx = up_index(x, p.w2, p.w3);
+          l2[pp * LG + r16] = acc[e] + l3[(sy * p.w3 + sx) * LG + r16];
+        }
+      }
+    }
+  }
+  stamp(p.stamps, 3);
+  __syncthreads();
+
+  // lat1 = L1 . tap1 + up(lat2) -> HBM, and max |lat1| of the image
+  float m = 0.f;
+  {
+    constexpr int JB = 6;
+    float4 bw[NK1];
+#pragma unroll
+    for (int k = 0; k < NK1; ++k) bw[k] = *reinterpret_cast<const float4*>(p.L1 + (size_t)co * (NK1 * 16) + 4 * g + 16 * k);
+    const int nt1 = (P1 + 15) / 16;
+    float* out = p.lat1 + (size_t)b * P1 * 128 + co;
+    for (int t0 = wave; t0 < nt1; t0 += NW * JB) {
+      float4 a[JB][NK1];
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const int px = min((t0 + NW * j) * 16 + r16, P1 - 1);
+#pragma unroll
+        for (int k = 0; k < NK1; ++k) a[j][k] = *reinterpret_cast<const float4*>(t1 + (size_t)px * (NK1 * 16) + 16 * k);
+      }
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const int t = t0 + NW * j;
+        if (t >= nt1) break;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < NK1; ++k) acc = mfma_k16(a[j][k], bw[k], acc);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int pp = t * 16 + 4 * g + e;
+          if (pp >= P1) continue;
+          const int y = pp / p.w1, x = pp - y * p.w1;
+          const int sy = up_index(y, p.h1, p.h2), sx = up_index(x, p.w1, p.w2);
+          const float v = acc[e] + l2[(sy * p.w2 + sx) * LG + r16];
+          out[(size_t)pp * 128] = v;
+          m = fmaxf(m, fabsf(v));
+        }
+      }
+    }
+  }
+  stamp(p.stamps, 4);
+  if (p.amax) {
+    m = wave_max(m);
+    if (lane == 0) amax_publish_img(p.amax, b, m);
+  }
+  stamp(p.stamps, 5);
+}
+
+}  // namespace
+
+size_t lateral_chain_lds_bytes(const LatChainArgs& a) {
+  const size_t P2 = (size_t)a.h2 * a.w2, P3 = (size_t)a.h3 * a.w3;
+  return (P3 * LG + std::max(P2, NW * P3) * LG) * sizeof(float);
+}
+
+bool lateral_chain_ok(const LatChainArgs& a) {
+  return a.c1 == 32 && a.c2 == 48 && a.c3 == 576 && a.h1 > 0 && a.w1 > 0 && a.h2 > 0 && a.w2 > 0 && a.h3 > 0 &&
+         a.w3 > 0 && a.h3 * a.w3 <= 16 * 8 && lateral_chain_lds_bytes(a) <= 64 * 1024;
+}
+
+hipError_t launch_lateral_chain(const LatChainArgs& a, int B, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (!lateral_chain_ok(a)) return hipErrorInvalidValue;
+  LatChainArgs q = a;
+  q.n = B;
+  const dim3 grid((unsigned)((B + 7) / 8 * 8), 128 / LG), block(NW * 64);
+  const size_t lds = lateral_chain_lds_bytes(a);
+  if (a.h3 * a.w3 <= 16 * 3) hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3>), grid, block, lds, st, q);
+  else hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8>), grid, block, lds, st, q);
+  return hipGetLastError();
+}
