@@ -245,15 +245,20 @@ hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles
                                 hipStream_t st);
 // LightweightFPN laterals 3 -> 2 -> 1 with the top-down adds in one launch
 // (lateral_chain.hip): taps t_i NHWC [N][h_i * w_i][c_i] (c_i = padded input
-// channels: 32, 48, 576; lateral 3 at most 128 pixels), weights L_i
-// [128][c_i] (no bias); writes lat1 [N][h1*w1][128]
-// and (amax != null) per-image max |lat1| at amax[n * kAmaxStride]
+// channels: 32, 48, 576; c_ir real ones; lateral 3 at most 128 pixels),
+// weights L_i [128][c_i] (no bias).  Writes lat1 fp32 [N][h1*w1][128], or with
+// lat1_split the f16 hi|lo rows of fpn0x_kernel, scaled per image by
+// fpn0x_exps(amax[n], bound) and the bound S1 m1 + S2 m2 + S3 m3 published at
+// amax[(N + n) * kAmaxStride] (S_i = max_co sum_k |L_i[co][k]|).
 struct LatChainArgs {
   const float *t1, *t2, *t3, *L1, *L2, *L3;
-  int c1, c2, c3, h1, w1, h2, w2, h3, w3;
+  int c1, c2, c3, c1r, c2r, c3r, h1, w1, h2, w2, h3, w3;
   int n;   // images (set by launch_lateral_chain)
   float* lat1;
-  float* amax;
+  _Float16* lat1_split;
+  float* amax;          // split: per-image slots, [0, N) max|tap0| (read), [N, 2N) the bound (published)
+  float S1, S2, S3;
+  int w_exp0, w_expE;
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 size_t lateral_chain_lds_bytes(const LatChainArgs& a);

@@ -188,6 +188,7 @@ struct kpd_plan {
   DevBneck bn[11];
   DevConv last;
   DevConv lat[4];
+  float lat_S[4] = {0.f, 0.f, 0.f, 0.f};   // max over output channels of sum |lateral weight| (lateral_chain bound)
   DevConv fpn0;
   DevConv fpn_lv[3];   // fpn_convs.1-3 (MobileNetV3Wrapper.forward only; the model's forward skips them)
   bool has_body = false, has_fpn = false, has_ca = false, has_hm = false;   // components registered
@@ -994,9 +995,22 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
   }
   }
   if (p->has_fpn) {
-  for (int i = 0; i < 4; ++i)
-    chk(pack_conv(p, "backbone.fpn.lateral_convs." + std::to_string(i) + ".weight", "", "", 0, 1, false,
-                  p->lat[i], missing));
+  for (int i = 0; i < 4; ++i) {
+    const std::string wn = "backbone.fpn.lateral_convs." + std::to_string(i) + ".weight";
+    chk(pack_conv(p, wn, "", "", 0, 1, false, p->lat[i], missing));
+    if (const HostT* lw = get(p, wn, missing)) {
+      const size_t cout = (size_t)lw->shape[0], cin = lw->data.size() / std::max<size_t>(cout, 1);
+      double smax = 0.0;
+      for (size_t o = 0; o < cout; ++o) {
+        double sum = 0.0;
+        for (size_t k = 0; k < cin; ++k) sum += std::fabs((double)lw->data[o * cin + k]);
+        smax = std::max(smax, sum);
+      }
+      float sf = (float)smax;
+      if ((double)sf < smax) sf = std::nextafter(sf, INFINITY);
+      p->lat_S[i] = sf;
+    }
+  }
   chk(pack_conv(p, "backbone.fpn.fpn_convs.0.0.weight", "", "backbone.fpn.fpn_convs.0.1", 1e-5, 3, false,
                 p->fpn0, missing));
   if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty()) chk(pack_fpn0x(p, p->fpn0, p->lat[0]));
@@ -1565,9 +1579,15 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   lc.L1 = static_cast<const float*>(p->lat[1].w); lc.L2 = static_cast<const float*>(p->lat[2].w);
   lc.L3 = static_cast<const float*>(p->lat[3].w);
   lc.c1 = pad16(kFpnIn[1]); lc.c2 = pad16(kFpnIn[2]); lc.c3 = pad16(kFpnIn[3]);
+  lc.c1r = kFpnIn[1]; lc.c2r = kFpnIn[2]; lc.c3r = kFpnIn[3];
+  lc.S1 = p->lat_S[1]; lc.S2 = p->lat_S[2]; lc.S3 = p->lat_S[3];
+  lc.w_exp0 = p->fpn0x.w_exp0; lc.w_expE = p->fpn0x.w_expE;
   lc.h1 = lh[1]; lc.w1 = lw[1]; lc.h2 = lh[2]; lc.w2 = lw[2]; lc.h3 = lh[3]; lc.w3 = lw[3];
   lc.lat1 = w.lat[1];
-  lc.amax = lin ? w.sc + (size_t)B * kAmaxStride : nullptr;
+  // split: lateral 1 goes straight to the hi|lo rows fpn0x_kernel reads (after the tap0 rows)
+  lc.lat1_split = lin ? reinterpret_cast<_Float16*>(reinterpret_cast<char*>(w.lat[0]) + (size_t)B * lh[0] * lw[0] * 64)
+                      : nullptr;
+  lc.amax = lin ? w.sc : nullptr;
   lc.stamps = take_stamps("stamps_latchain_0", (size_t)8 * ((B + 7) / 8 * 8));
   const bool chain = !no_chain && !p->keep_laterals && !p->lat[1].bf16 && !p->lat[2].bf16 && !p->lat[3].bf16 &&
                      p->lat[1].cin_p == lc.c1 && p->lat[2].cin_p == lc.c2 && p->lat[3].cin_p == lc.c3 &&
@@ -1582,8 +1602,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       char* base = reinterpret_cast<char*>(w.lat[0]);
       HIP_TRY(launch_split_rows(taps[0], B, (long)lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
                                 base, st));
-      HIP_TRY(launch_split_rows(w.lat[1], B, (long)lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
-                                p->fpn0x.w_expE, base + (size_t)B * lh[0] * lw[0] * 64, st));
+      if (!chain)
+        HIP_TRY(launch_split_rows(w.lat[1], B, (long)lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
+                                  p->fpn0x.w_expE, base + (size_t)B * lh[0] * lw[0] * 64, st));
       continue;
     }
     if (i == 0 && L.cin_p <= 32) {   // the 16-channel stem tap: a 403 MB/step stream, not a GEMM

@@ -44,18 +44,31 @@ __device__ __forceinline__ f32x4 mfma_k16(const float4 a, const float4 b, f32x4 
 
 // NK1 / NK2 / NK3: 16-channel K chunks of laterals 1 / 2 / 3 (the model's 24
 // -> 32, 48 and 576 input channels); T3: lateral-3 tiles (at most 16 * T3
-// pixels).  Eight waves; every phase issues all its independent loads before
-// its MFMAs, so a phase costs about one memory round trip: the chain is
-// latency, not bandwidth (a 256x192 image's whole chain reads 0.3 MB).
+// pixels); T1: lateral-1 tiles per wave and load batch.  Eight waves; every phase
+// issues all its independent loads before its MFMAs, so a phase costs about
+// one memory round trip: the chain is latency (and fp32-MFMA rate), not
+// bandwidth (a 256x192 image's whole chain reads 0.3 MB).
+//
+// SPLIT: lateral 1 leaves as the f16 hi|lo rows fpn0x_kernel reads (the
+// layout of split_rows_kernel), scaled by 2^a_l from fpn0x_exps(max|tap0|,
+// bound).  The bound is S1 m1 + S2 m2 + S3 m3 >= max|lateral 1| (S_i = max
+// over output channels of sum |L_i|, m_i = max|tap_i| of the image): every
+// workgroup of the image reads all of its taps, so all eight compute the same
+// bound without talking to each other, and it is published in place of the
+// max (slot amax[n * kAmaxStride]) for the consumers' unscale.  A bound
+// looser than the max only lowers the split's precision floor, which sits
+// ~2^-39 of the largest scaled operand: 2^12 of slack still leaves it below
+// fp32 rounding.
 constexpr int NW = 8;
 
-template <int NK1, int NK2, int NK3, int T3>
+template <int NK1, int NK2, int NK3, int T3, int T1, bool SPLIT>
 __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainArgs p) {
   extern __shared__ __attribute__((aligned(16))) float lsm[];
   const int P1 = p.h1 * p.w1, P2 = p.h2 * p.w2, P3 = p.h3 * p.w3;
   float* l3 = lsm;                      // [P3][16]
   float* l2 = l3 + P3 * LG;             // [P2][16]
   float* red = l2;                      // [NW][P3][16] lat3 partials (dead before l2 is written)
+  float* mx = l2 + max(P2, NW * P3) * LG;   // [3][NW] per-wave tap maxima
   // grid (B rounded up to 8, 8): workgroup id b + Bp * cg sits on XCD b % 8,
   // so an image's 8 channel groups share one L2 and its taps leave HBM once
   const int b = blockIdx.x, cg = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -64,30 +77,45 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
   const float* t1 = p.t1 + (size_t)b * P1 * (NK1 * 16) + 4 * g;
   const float* t2 = p.t2 + (size_t)b * P2 * (NK2 * 16) + 4 * g;
   const float* t3 = p.t3 + (size_t)b * P3 * (NK3 * 16) + 4 * g;
+  // max |x| over the real input channels (c0 = this float4's first channel)
+  auto amax4 = [](float m, const float4 v, int c0, int creal) {
+    if (c0 + 0 < creal) m = fmaxf(m, fabsf(v.x));
+    if (c0 + 1 < creal) m = fmaxf(m, fabsf(v.y));
+    if (c0 + 2 < creal) m = fmaxf(m, fabsf(v.z));
+    if (c0 + 3 < creal) m = fmaxf(m, fabsf(v.w));
+    return m;
+  };
+  float m1 = 0.f, m2 = 0.f, m3 = 0.f;
   stamp(p.stamps, 0);
 
   // lat3: every tile at once, K chunks q = wave + NW * u (partials added in wave order)
   {
-    constexpr int U3 = (NK3 + NW - 1) / NW;
+    constexpr int U3 = (NK3 + NW - 1) / NW, UB = T3 <= 3 ? 3 : 1;   // K chunks per wave, per load batch
     const int nt3 = (P3 + 15) / 16;
     const float* brow = p.L3 + (size_t)co * (NK3 * 16) + 4 * g;
-    float4 bb[U3], a[U3][T3];
-#pragma unroll
-    for (int u = 0; u < U3; ++u) {
-      const int q = min(wave + NW * u, NK3 - 1);
-      bb[u] = *reinterpret_cast<const float4*>(brow + q * 16);
-#pragma unroll
-      for (int t = 0; t < T3; ++t)
-        a[u][t] = *reinterpret_cast<const float4*>(t3 + (size_t)min(t * 16 + r16, P3 - 1) * (NK3 * 16) + q * 16);
-    }
     f32x4 acc[T3];
 #pragma unroll
     for (int t = 0; t < T3; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < U3; ++u)
-      if (wave + NW * u < NK3)
+    for (int u0 = 0; u0 < U3; u0 += UB) {
+      float4 bb[UB], a[UB][T3];
 #pragma unroll
-        for (int t = 0; t < T3; ++t) acc[t] = mfma_k16(a[u][t], bb[u], acc[t]);
+      for (int u = 0; u < UB; ++u) {
+        const int q = min(wave + NW * (u0 + u), NK3 - 1);
+        bb[u] = *reinterpret_cast<const float4*>(brow + q * 16);
+#pragma unroll
+        for (int t = 0; t < T3; ++t)
+          a[u][t] = *reinterpret_cast<const float4*>(t3 + (size_t)min(t * 16 + r16, P3 - 1) * (NK3 * 16) + q * 16);
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+        if (u0 + u < U3 && wave + NW * (u0 + u) < NK3)
+#pragma unroll
+          for (int t = 0; t < T3; ++t) {
+            acc[t] = mfma_k16(a[u][t], bb[u], acc[t]);
+            if (SPLIT) m3 = amax4(m3, a[u][t], (wave + NW * (u0 + u)) * 16 + 4 * g, p.c3r);
+          }
+    }
 #pragma unroll
     for (int t = 0; t < T3; ++t)
 #pragma unroll
@@ -95,6 +123,28 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
         const int pp = t * 16 + 4 * g + e;
         if (t < nt3 && pp < P3) red[(wave * P3 + pp) * LG + r16] = acc[t][e];
       }
+  }
+  if (SPLIT) {
+    // max |tap1| of the image over the real channels: wave w scans pixels w, w + NW, ...
+    // (batches of 6 pixel rows per lane, loads issued together)
+    for (int px0 = wave * 16 + r16; px0 < P1; px0 += 6 * NW * 16) {
+      float4 v[6][NK1];
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int k = 0; k < NK1; ++k)
+          v[j][k] = *reinterpret_cast<const float4*>(t1 + (size_t)min(px0 + j * NW * 16, P1 - 1) * (NK1 * 16) + 16 * k);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int k = 0; k < NK1; ++k) m1 = amax4(m1, v[j][k], 16 * k + 4 * g, p.c1r);
+    }
+    m1 = wave_max(m1);
+    m3 = wave_max(m3);
+    if (lane == 0) {
+      mx[wave] = m1;
+      mx[2 * NW + wave] = m3;
+    }
   }
   stamp(p.stamps, 1);
   __syncthreads();
@@ -128,7 +178,10 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
         if (t >= nt2) break;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < NK2; ++k) acc = mfma_k16(a[j][k], bw[k], acc);
+        for (int k = 0; k < NK2; ++k) {
+          acc = mfma_k16(a[j][k], bw[k], acc);
+          if (SPLIT) m2 = amax4(m2, a[j][k], 16 * k + 4 * g, p.c2r);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int pp = t * 16 + 4 * g + e;
@@ -140,13 +193,34 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
       }
     }
   }
+  if (SPLIT) {
+    m2 = wave_max(m2);
+    if (lane == 0) mx[NW + wave] = m2;
+  }
   stamp(p.stamps, 3);
   __syncthreads();
 
-  // lat1 = L1 . tap1 + up(lat2) -> HBM, and max |lat1| of the image
-  float m = 0.f;
+  // lat1 = L1 . tap1 + up(lat2) -> HBM (fp32, or split by the image's bound)
+  float s_l = 1.f;
+  _Float16* outs = nullptr;
+  if constexpr (SPLIT) {
+    float M1 = mx[0], M2 = mx[NW], M3 = mx[2 * NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      M1 = fmaxf(M1, mx[w]);
+      M2 = fmaxf(M2, mx[NW + w]);
+      M3 = fmaxf(M3, mx[2 * NW + w]);
+    }
+    const float bound = fmaf(p.S1, M1, fmaf(p.S2, M2, p.S3 * M3));
+    int a_f, a_l, P;
+    fpn0x_exps(p.amax[(size_t)b * kAmaxStride], bound, p.w_exp0, p.w_expE, &a_f, &a_l, &P);
+    s_l = ldexpf(1.f, a_l);
+    if (tid == 0) amax_publish_img(p.amax + (size_t)p.n * kAmaxStride, b, bound);
+    // hi|lo rows: pixel pp at halves [pp][2 * 128]; channel co in group co / 32: hi at +co % 32, lo 32 further
+    outs = p.lat1_split + (size_t)b * P1 * 256 + (co >> 5) * 64 + (co & 31);
+  }
   {
-    constexpr int JB = 6;
+    constexpr int JB = T1;
     float4 bw[NK1];
 #pragma unroll
     for (int k = 0; k < NK1; ++k) bw[k] = *reinterpret_cast<const float4*>(p.L1 + (size_t)co * (NK1 * 16) + 4 * g + 16 * k);
@@ -174,17 +248,19 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
           const int y = pp / p.w1, x = pp - y * p.w1;
           const int sy = up_index(y, p.h1, p.h2), sx = up_index(x, p.w1, p.w2);
           const float v = acc[e] + l2[(sy * p.w2 + sx) * LG + r16];
-          out[(size_t)pp * 128] = v;
-          m = fmaxf(m, fabsf(v));
+          if constexpr (SPLIT) {
+            const float xs = v * s_l;
+            const _Float16 hi = (_Float16)xs;
+            outs[(size_t)pp * 256] = hi;
+            outs[(size_t)pp * 256 + 32] = (_Float16)(xs - (float)hi);
+          } else {
+            out[(size_t)pp * 128] = v;
+          }
         }
       }
     }
   }
   stamp(p.stamps, 4);
-  if (p.amax) {
-    m = wave_max(m);
-    if (lane == 0) amax_publish_img(p.amax, b, m);
-  }
   stamp(p.stamps, 5);
 }
 
@@ -192,12 +268,13 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
 
 size_t lateral_chain_lds_bytes(const LatChainArgs& a) {
   const size_t P2 = (size_t)a.h2 * a.w2, P3 = (size_t)a.h3 * a.w3;
-  return (P3 * LG + std::max(P2, NW * P3) * LG) * sizeof(float);
+  return (P3 * LG + std::max(P2, NW * P3) * LG + 3 * NW) * sizeof(float);
 }
 
 bool lateral_chain_ok(const LatChainArgs& a) {
   return a.c1 == 32 && a.c2 == 48 && a.c3 == 576 && a.h1 > 0 && a.w1 > 0 && a.h2 > 0 && a.w2 > 0 && a.h3 > 0 &&
-         a.w3 > 0 && a.h3 * a.w3 <= 16 * 8 && lateral_chain_lds_bytes(a) <= 64 * 1024;
+         a.w3 > 0 && a.h3 * a.w3 <= 16 * 8 && lateral_chain_lds_bytes(a) <= 64 * 1024 &&
+         (!a.lat1_split || a.amax);
 }
 
 hipError_t launch_lateral_chain(const LatChainArgs& a, int B, hipStream_t st) {
@@ -207,7 +284,13 @@ hipError_t launch_lateral_chain(const LatChainArgs& a, int B, hipStream_t st) {
   q.n = B;
   const dim3 grid((unsigned)((B + 7) / 8 * 8), 128 / LG), block(NW * 64);
   const size_t lds = lateral_chain_lds_bytes(a);
-  if (a.h3 * a.w3 <= 16 * 3) hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3>), grid, block, lds, st, q);
-  else hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8>), grid, block, lds, st, q);
+  const bool small = a.h3 * a.w3 <= 16 * 3;
+  if (a.lat1_split) {
+    if (small) hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3, 6, true>), grid, block, lds, st, q);
+    else hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8, 6, true>), grid, block, lds, st, q);
+  } else {
+    if (small) hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3, 6, false>), grid, block, lds, st, q);
+    else hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8, 6, false>), grid, block, lds, st, q);
+  }
   return hipGetLastError();
 }
