@@ -943,18 +943,36 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
   // LDS: [xs: npx_in x cin_p] [es: npx_in x CS] [ds: TH*Wo x CS] [weT: cin_p x CS] [wds: K*K x CS] [wpT: CS x cout_p]
   float* xs = sm;
   float* es = xs + npx_in * cin_p;
-  float* ds = es + npx_in * CS;
+  float* ds = es + (npx_in + 3) / 4 * 4 * CS;
   float* weT = ds + a.TH * Wo * CS;
   float* wds = weT + cin_p * CS;
   float* wpT = wds + K * K * CS;
+  float* sb = wpT + CS * cout_p;   // [be slice: CS][bd slice: CS]
+  // es pixel p lives at row esw(p): the depthwise threads of one ds_read_b128
+  // lane group read pixels XT * S apart, which would share banks; the swizzle
+  // (a permutation within aligned groups of 4 rows, es padded to a multiple of
+  // 4) spreads them over the 4 bank quarters
+  constexpr int SWS = S == 2 ? 3 : 2;
+  auto esw = [](int p) { return p ^ ((p >> SWS) & 3); };
   // the input rows of the tile (zero outside the image)
   const float* xg = a.x + (size_t)n * a.Hi * Wi * cin_p;
-  const int cq_in = cin_p / 4;
-  for (int i = tid; i < npx_in * cq_in; i += 256) {
-    const int px = i / cq_in, q = i - px * cq_in, iy = iy0 + px / Wi;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (iy >= 0 && iy < a.Hi) v = *reinterpret_cast<const float4*>(xg + ((size_t)iy * Wi + px % Wi) * cin_p + q * 4);
-    reinterpret_cast<float4*>(xs)[i] = v;
+  stamp(a.stamps, 0);
+  // (batches of 8 loads per thread issued together, then the LDS stores)
+  const int cq_in = cin_p / 4, nxq = npx_in * cq_in;
+  for (int i0 = 0; i0 < nxq; i0 += 8 * 256) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = min(i0 + u * 256 + tid, nxq - 1);
+      const int px = i / cq_in, q = i - px * cq_in, iy = iy0 + px / Wi;
+      v[u] = *reinterpret_cast<const float4*>(xg + ((size_t)min(max(iy, 0), a.Hi - 1) * Wi + px % Wi) * cin_p + q * 4);
+      if (iy < 0 || iy >= a.Hi) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256 + tid;
+      if (i < nxq) reinterpret_cast<float4*>(xs)[i] = v[u];
+    }
   }
   // project accumulators: unit = (pixel pair, 8 output channels)
   const int nco8 = cout_p / 8, npair = (npx + 1) / 2, units = npair * nco8;
@@ -974,8 +992,13 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
   // measured 84 vs 51 us: more LDS reads per FMA; not kept.)
   constexpr int PE = 4, PP = 4;   // cin_p * CS <= 1024, CS * cout_p <= 1024 (fir_pick_rows)
   float pe[PE], pp[PP];
-  float4 pd = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 pd = make_float4(0.f, 0.f, 0.f, 0.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
   auto prefetch = [&](int c0) {
+    // the slice's expand / depthwise biases ride along (no global round trip inside a phase)
+    if (tid >= 256 - 2 * CQ) {
+      const int v = tid - (256 - 2 * CQ);
+      pb = *reinterpret_cast<const float4*>((v < CQ ? a.be : a.bd) + c0 + (v % CQ) * 4);
+    }
 #pragma unroll
     for (int u = 0; u < PE; ++u) {
       const int i = tid + u * 256, c = i / cin_p, k = i - c * cin_p;
@@ -1000,6 +1023,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
       if (i < cin_p * CS) weT[k * CS + c] = pe[u];
     }
     if (tid < K * K * CQ) reinterpret_cast<float4*>(wds)[tid] = pd;
+    if (tid >= 256 - 2 * CQ) reinterpret_cast<float4*>(sb)[tid - (256 - 2 * CQ)] = pb;
 #pragma unroll
     for (int u = 0; u < PP; ++u) {
       const int i = tid + u * 256, co = i / CS, c = i - co * CS;
@@ -1007,17 +1031,18 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
     }
     if (c0 + CS < a.Ep) prefetch(c0 + CS);
     __syncthreads();
+    if (c0 == 0) stamp(a.stamps, 1);
     // expand: 4 pixels x 4 channels per thread, weights from LDS
     const int pg_n = (npx_in + 3) / 4;
     for (int i = tid; i < pg_n * CQ; i += 256) {
       const int pg = i / CQ, q = i - pg * CQ;
-      const float4 b = *reinterpret_cast<const float4*>(a.be + c0 + q * 4);
+      const float4 b = reinterpret_cast<const float4*>(sb)[q];
       float acc_e[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { acc_e[r][0] = b.x; acc_e[r][1] = b.y; acc_e[r][2] = b.z; acc_e[r][3] = b.w; }
       int pxr[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pxr[r] = min(pg * 4 + r, npx_in - 1);
+      for (int r = 0; r < 4; ++r) pxr[r] = min(r * pg_n + pg, npx_in - 1);   // pixels pg_n apart: conflict-free xs reads
       for (int k = 0; k < cin_p; k += 4) {
         float4 xv[4], wv[4];
 #pragma unroll
@@ -1036,17 +1061,18 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int px = pg * 4 + r;
+        const int px = r * pg_n + pg;
         if (px >= npx_in) break;
         const int iy = iy0 + px / Wi;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);   // the depthwise zero padding of the expanded tensor
         if (iy >= 0 && iy < a.Hi)
           v = make_float4(kpd_act(acc_e[r][0], a.act_e), kpd_act(acc_e[r][1], a.act_e),
                           kpd_act(acc_e[r][2], a.act_e), kpd_act(acc_e[r][3], a.act_e));
-        reinterpret_cast<float4*>(es)[px * CQ + q] = v;
+        reinterpret_cast<float4*>(es)[esw(px) * CQ + q] = v;
       }
     }
     __syncthreads();
+    if (c0 == 0) stamp(a.stamps, 2);
     // depthwise: 4 consecutive output columns x 4 channels per thread
     constexpr int XT = 4, NC = (XT - 1) * S + K;
     const int wx = (Wo + XT - 1) / XT;
@@ -1062,7 +1088,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           const int ix = ix0 + c;
-          col[c] = (ix >= 0 && ix < Wi) ? reinterpret_cast<const float4*>(es)[(ly * Wi + ix) * CQ + q]
+          col[c] = (ix >= 0 && ix < Wi) ? reinterpret_cast<const float4*>(es)[esw(ly * Wi + ix) * CQ + q]
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
@@ -1076,7 +1102,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
           }
         }
       }
-      const float4 b = *reinterpret_cast<const float4*>(a.bd + c0 + q * 4);
+      const float4 b = reinterpret_cast<const float4*>(sb)[CQ + q];
 #pragma unroll
       for (int o = 0; o < XT; ++o) {
         if (ox0 + o >= Wo) break;
@@ -1087,6 +1113,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
       }
     }
     __syncthreads();
+    if (c0 == 0) stamp(a.stamps, 3);
     // project: fold this slice into the accumulators
     if (has_unit) {
 #pragma unroll
@@ -1108,6 +1135,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
       }
     }
   }
+  stamp(a.stamps, 4);
   if (!has_unit) return;
   const float4 b0 = *reinterpret_cast<const float4*>(a.bp + u_co), b1 = *reinterpret_cast<const float4*>(a.bp + u_co + 4);
   const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -1128,7 +1156,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
     float* op = a.out + (((size_t)n * a.Ho + oy) * Wo + ox) * cout_p + u_co;
     *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(op + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  }
+  }  stamp(a.stamps, 5);
 }
 
 // Squeeze-excitation, one 1024-thread workgroup (16 waves) per kSeImages
@@ -1371,8 +1399,8 @@ hipError_t launch_channel_stats(const float* x, int N, int HW, int Cp, int tiles
 
 size_t fir_lds_bytes(const FirArgs& a, int K, int S) {
   const size_t THin = (size_t)(a.TH - 1) * S + K;
-  return 4 * (THin * a.Wi * a.cin_p + THin * a.Wi * FIR_CS + (size_t)a.TH * a.Wo * FIR_CS + (size_t)a.cin_p * FIR_CS +
-              (size_t)K * K * FIR_CS + (size_t)FIR_CS * a.cout_p);
+  return 4 * (THin * a.Wi * a.cin_p + (THin * a.Wi + 3) / 4 * 4 * FIR_CS + (size_t)a.TH * a.Wo * FIR_CS + (size_t)a.cin_p * FIR_CS +
+              (size_t)K * K * FIR_CS + (size_t)FIR_CS * a.cout_p + 2 * FIR_CS);
 }
 
 int fir_pick_rows(FirArgs& a, int K, int S) {

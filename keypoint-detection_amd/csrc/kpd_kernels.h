@@ -155,6 +155,7 @@ struct FirArgs {
   float* out;            // NHWC [N][Ho][Wo][cout_p]
   int Ho, Wo, res;       // res: add x (stride 1, cin_p == cout_p)
   int TH;                // output rows per workgroup (host-chosen)
+  unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 size_t fir_lds_bytes(const FirArgs& a, int K, int S);
 int fir_pick_rows(FirArgs& a, int K, int S);   // sets a.TH; 0 when the layer does not fit

@@ -1484,6 +1484,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       fa.out = w.o[i]; fa.Ho = ho; fa.Wo = wo;
       fa.res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
       if (fir_pick_rows(fa, bn.dw.k, bn.dw.s)) {
+        fa.stamps = take_stamps("stamps_fir_" + std::to_string(i), (size_t)((ho + fa.TH - 1) / fa.TH) * B);
         HIP_TRY(launch_fir(fa, B, bn.dw.k, bn.dw.s, st));
         x = w.o[i];
         if (i + 1 == 3) taps[1] = x;

@@ -61,7 +61,7 @@ def forwards(rows, key):
     rows.sort(key=key)
     fw, cur = [], None
     for r in rows:
-        if r[1].startswith("stem_kernel"):
+        if r[1].startswith("stem_kernel") or r[1].startswith("stem_band_kernel"):
             cur = []
             fw.append(cur)
         if cur is not None:
