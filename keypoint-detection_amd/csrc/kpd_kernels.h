@@ -260,6 +260,9 @@ struct LatChainArgs {
   float* amax;          // split: per-image slots, [0, N) max|tap0| (read), [N, 2N) the bound (published)
   float S1, S2, S3;
   int w_exp0, w_expE;
+  const float* t0;      // split: optional stem tap [N][P0][16] -> t0_split hi|lo rows (2^a_f), else null
+  _Float16* t0_split;
+  int P0;
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
 };
 size_t lateral_chain_lds_bytes(const LatChainArgs& a);

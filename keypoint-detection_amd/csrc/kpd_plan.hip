@@ -1589,6 +1589,12 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   lc.lat1_split = lin ? reinterpret_cast<_Float16*>(reinterpret_cast<char*>(w.lat[0]) + (size_t)B * lh[0] * lw[0] * 64)
                       : nullptr;
   lc.amax = lin ? w.sc : nullptr;
+  static const bool no_chain_t0 = getenv("KPD_NO_CHAIN_TAP0") != nullptr;   // A/B: tap0 split as its own launch
+  if (lin && !no_chain_t0) {
+    lc.t0 = taps[0];
+    lc.t0_split = reinterpret_cast<_Float16*>(w.lat[0]);
+    lc.P0 = lh[0] * lw[0];
+  }
   lc.stamps = take_stamps("stamps_latchain_0", (size_t)8 * ((B + 7) / 8 * 8));
   const bool chain = !no_chain && !p->keep_laterals && !p->lat[1].bf16 && !p->lat[2].bf16 && !p->lat[3].bf16 &&
                      p->lat[1].cin_p == lc.c1 && p->lat[2].cin_p == lc.c2 && p->lat[3].cin_p == lc.c3 &&
@@ -1601,8 +1607,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     const float* res = i < 3 ? w.lat[i + 1] : nullptr;
     if (i == 0 && lin) {   // no lateral 0: tap0 and lateral 1 go to the split layouts fpn0x_kernel reads
       char* base = reinterpret_cast<char*>(w.lat[0]);
-      HIP_TRY(launch_split_rows(taps[0], B, (long)lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
-                                base, st));
+      if (!chain || !lc.t0)
+        HIP_TRY(launch_split_rows(taps[0], B, (long)lh[0] * lw[0], 16, w.sc, 0, p->fpn0x.w_exp0, p->fpn0x.w_expE,
+                                  base, st));
       if (!chain)
         HIP_TRY(launch_split_rows(w.lat[1], B, (long)lh[1] * lw[1], 128, w.sc, 1, p->fpn0x.w_exp0,
                                   p->fpn0x.w_expE, base + (size_t)B * lh[0] * lw[0] * 64, st));

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
   __syncthreads();
 
   // lat1 = L1 . tap1 + up(lat2) -> HBM (fp32, or split by the image's bound)
-  float s_l = 1.f;
+  float s_l = 1.f, s_f = 1.f;
   _Float16* outs = nullptr;
   if constexpr (SPLIT) {
     float M1 = mx[0], M2 = mx[NW], M3 = mx[2 * NW];
@@ -215,6 +215,7 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
     int a_f, a_l, P;
     fpn0x_exps(p.amax[(size_t)b * kAmaxStride], bound, p.w_exp0, p.w_expE, &a_f, &a_l, &P);
     s_l = ldexpf(1.f, a_l);
+    s_f = ldexpf(1.f, a_f);
     if (tid == 0) amax_publish_img(p.amax + (size_t)p.n * kAmaxStride, b, bound);
     // hi|lo rows: pixel pp at halves [pp][2 * 128]; channel co in group co / 32: hi at +co % 32, lo 32 further
     outs = p.lat1_split + (size_t)b * P1 * 256 + (co >> 5) * 64 + (co & 31);
@@ -261,6 +262,43 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
     }
   }
   stamp(p.stamps, 4);
+  if constexpr (SPLIT) {
+    // the stem tap's split rows (split_rows_kernel's layout for 16 channels:
+    // [hi16 | lo16] per pixel) with 2^a_f: channel group cg converts its
+    // eighth of the image's pixels, 8 channels per item, loads batched; this
+    // streams beside the latency-bound chain instead of as its own launch
+    if (p.t0) {
+      const int P0 = p.P0, n8 = P0 * 2, per = (n8 + 7) / 8, i0 = cg * per, i1 = min(i0 + per, n8);
+      const float* src = p.t0 + (size_t)b * P0 * 16;
+      _Float16* dst = p.t0_split + (size_t)b * P0 * 32;
+      typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+      for (int j0 = i0 + tid; j0 < i1; j0 += 4 * NW * 64) {
+        float4 u[4][2];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int j = min(j0 + v * NW * 64, i1 - 1), px = j >> 1, c = (j & 1) * 8;
+          u[v][0] = *reinterpret_cast<const float4*>(src + (size_t)px * 16 + c);
+          u[v][1] = *reinterpret_cast<const float4*>(src + (size_t)px * 16 + c + 4);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int j = j0 + v * NW * 64, px = j >> 1, c = (j & 1) * 8;
+          if (j >= i1) continue;
+          const float x[8] = {u[v][0].x, u[v][0].y, u[v][0].z, u[v][0].w, u[v][1].x, u[v][1].y, u[v][1].z, u[v][1].w};
+          f16x8v hi, lo;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xs = x[e] * s_f;
+            hi[e] = (_Float16)xs;
+            lo[e] = (_Float16)(xs - (float)hi[e]);
+          }
+          _Float16* o = dst + (size_t)px * 32 + c;
+          *reinterpret_cast<f16x8v*>(o) = hi;
+          *reinterpret_cast<f16x8v*>(o + 16) = lo;
+        }
+      }
+    }
+  }
   stamp(p.stamps, 5);
 }
 
