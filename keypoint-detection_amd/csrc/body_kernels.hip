@@ -458,8 +458,9 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 // in LDS in wave order (deterministic, independent of the batch).  The first
 // D chunks' loads do not depend on s and are issued before the excitation, so
 // their latency hides under it; each chunk's slot is refilled D chunks ahead.
-template <int MT, int NTT>
-__global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
+template <int MT, int NTT, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
+  constexpr int NTH = NWV * 64;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int NT = NTT * 16, MP = MT * 16;
   constexpr int D = (28 / (MT + NTT)) < 1 ? 1 : ((28 / (MT + NTT)) > 4 ? 4 : 28 / (MT + NTT));
@@ -467,17 +468,17 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
   const int Ep = a.Ep, Po = a.Po;
   float* sS = sm;                    // [Ep] excitation
   float* hid = sS + Ep;              // [256]
-  float* red = hid + 256;            // [4][MP][NT] partial tiles / SE scratch
+  float* red = hid + 256;            // [NWV][MP][NT] partial tiles / SE scratch
   stamp(a.stamps, 0);
   const int r = lane & 15, g = lane >> 4;
   // rows of this workgroup: [m0, m0 + MP) of the image (blockIdx.z splits M)
   const int m0 = blockIdx.z * MP, Pr = min(MP, Po - m0);
   const float* dbase = a.d + ((size_t)n * Po + m0) * Ep;
-  const int nkc = Ep / 16, ncw = (nkc - wave + 3) / 4;   // this wave's k chunks: wave + 4 t
+  const int nkc = Ep / 16, ncw = (nkc - wave + NWV - 1) / NWV;   // this wave's k chunks: wave + NWV t
   float4 av[D][MT], bv[D][NTT];
   auto load_chunk = [&](int t, float4* a4, float4* b4) {
     if (t < ncw) {
-      const int k = (wave + 4 * t) * 16 + g * 4;
+      const int k = (wave + NWV * t) * 16 + g * 4;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int px = mt * 16 + r;
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
 #pragma unroll
   for (int dd = 0; dd < D; ++dd) load_chunk(dd, av[dd], bv[dd]);
   if (a.sesc) {   // precomputed excitation
-    for (int c = tid; c < Ep / 4; c += 256)
+    for (int c = tid; c < Ep / 4; c += NTH)
       reinterpret_cast<float4*>(sS)[c] = reinterpret_cast<const float4*>(a.sesc + (size_t)n * Ep)[c];
     __syncthreads();
   } else {
@@ -499,19 +500,19 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
     const int npart = a.nsl * a.sq;
     const float* part = a.part + (size_t)n * npart;
     {
-      constexpr int NP = 6;   // npart / 4 <= 1536 (kSePartFloats / 4 / ... checked at launch)
+      constexpr int NP = 6 * 256 / NTH;   // npart / 4 <= 1536 (kSePartFloats / 4 / ... checked at launch)
       float4 v[NP];
 #pragma unroll
       for (int u = 0; u < NP; ++u)   // clamped (unconditional) loads keep v in registers
-        v[u] = reinterpret_cast<const float4*>(part)[min(tid + u * 256, npart / 4 - 1)];
+        v[u] = reinterpret_cast<const float4*>(part)[min(tid + u * NTH, npart / 4 - 1)];
 #pragma unroll
       for (int u = 0; u < NP; ++u) {
-        const int i = tid + u * 256;
+        const int i = tid + u * NTH;
         if (i < npart / 4) reinterpret_cast<float4*>(red)[i] = v[u];
       }
     }
     __syncthreads();
-    for (int j = tid; j < a.sq; j += 256) {
+    for (int j = tid; j < a.sq; j += NTH) {
       float h = 0.f;
       for (int s2 = 0; s2 < a.nsl; ++s2) h += red[s2 * a.sq + j];
       hid[j] = fmaxf(h + a.b1[j], 0.f);
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
       const int nq4 = a.C / 4, ngrp = max(1, min(16, 256 / nq4)), items = nq4 * ngrp;
       const int jper = (a.sq + ngrp - 1) / ngrp;
       float* fsum = red;   // [ngrp][C]
-      for (int it = tid; it < items; it += 256) {
+      for (int it = tid; it < items; it += NTH) {
         const int q = it % nq4, gi = it / nq4, j0 = gi * jper, j1 = min(a.sq, j0 + jper);
         float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
         constexpr int JU = 16;
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
         reinterpret_cast<float4*>(fsum + (size_t)gi * a.C)[q] = acc4;
       }
       __syncthreads();
-      for (int c = tid; c < Ep; c += 256) {
+      for (int c = tid; c < Ep; c += NTH) {
         float t = 0.f;
         if (c < a.C)
           for (int gi = 0; gi < ngrp; ++gi) t += fsum[(size_t)gi * a.C + c];
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
     for (int dd = 0; dd < D; ++dd) {
       const int t = t0 + dd;
       if (t < ncw) {
-        const float4 sv = *reinterpret_cast<const float4*>(sS + (wave + 4 * t) * 16 + g * 4);
+        const float4 sv = *reinterpret_cast<const float4*>(sS + (wave + NWV * t) * 16 + g * 4);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const float4 x4 = make_float4(av[dd][mt].x * sv.x, av[dd][mt].y * sv.y, av[dd][mt].z * sv.z,
@@ -594,15 +595,15 @@ __global__ __launch_bounds__(256) void seproj_kernel(const SeProjArgs a) {
       for (int i = 0; i < 4; ++i) rw[(mt * 16 + g * 4 + i) * NT + nt * 16 + r] = acc[mt][nt][i];
   __syncthreads();
   stamp(a.stamps, 3);
-  // (4) sum the 4 waves in order, bias, residual; 4 channels per thread
+  // (4) sum the NWV waves in order, bias, residual; 4 channels per thread
   constexpr int NQ = NT / 4;
   float* out = a.out + ((size_t)n * Po + m0) * a.cout_p + o0;
   const float* res = a.res ? a.res + ((size_t)n * Po + m0) * a.cout_p + o0 : nullptr;
-  for (int i = tid; i < Pr * NQ; i += 256) {
+  for (int i = tid; i < Pr * NQ; i += NTH) {
     const int px = i / NQ, q = i - px * NQ;
     float4 v = *reinterpret_cast<const float4*>(red + px * NT + q * 4);
 #pragma unroll
-    for (int w = 1; w < 4; ++w) {
+    for (int w = 1; w < NWV; ++w) {
       const float4 t = *reinterpret_cast<const float4*>(red + ((size_t)w * MP + px) * NT + q * 4);
       v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
     }
@@ -1495,12 +1496,23 @@ hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
   const int msplit = mt_all == 12 ? std::max(1, msplit_env) : 1;
   const int mt = (mt_all + msplit - 1) / msplit;
   SeProjArgs b = a;
-  const size_t lds_m = 4 * ((size_t)a.Ep + 256 + std::max({(size_t)4 * mt * 16 * a.NT, (size_t)a.nsl * a.sq,
+  // the 48-pixel maps (3 row tiles): eight waves split the project's K
+  // chunks (one wave per SIMD at four leaves the fp32-MFMA K loop exposed):
+  // 12.1 -> 9.6 us per launch.  The 192-pixel maps (6 row tiles per
+  // workgroup) measured 13.5 -> 16.9 us with eight, so they keep four.
+  // KPD_SEPROJ_NWV = 4 / 8 forces one (A/B).
+  static const int nwv_env = getenv("KPD_SEPROJ_NWV") ? atoi(getenv("KPD_SEPROJ_NWV")) : 0;
+  const int nwv = nwv_env == 4 || nwv_env == 8 ? nwv_env : (mt == 3 ? 8 : 4);
+  const size_t lds_m = 4 * ((size_t)a.Ep + 256 + std::max({(size_t)nwv * mt * 16 * a.NT, (size_t)a.nsl * a.sq,
                                                              std::max<size_t>(1, std::min<size_t>(16, 256 / (a.C / 4))) * a.C}));
   if (lds_m > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(a.cout_p / a.NT, N, msplit);
   const int ntt = a.NT / 16;
-#define SEP(M, T) hipLaunchKernelGGL((seproj_kernel<M, T>), grid, dim3(256), lds_m, st, b)
+#define SEP(M, T)                                                                                   \
+  do {                                                                                              \
+    if (nwv == 8) hipLaunchKernelGGL((seproj_kernel<M, T, 8>), grid, dim3(512), lds_m, st, b);     \
+    else hipLaunchKernelGGL((seproj_kernel<M, T, 4>), grid, dim3(256), lds_m, st, b);              \
+  } while (0)
   if (mt == 3 && ntt == 1) SEP(3, 1);
   else if (mt == 3 && ntt == 2) SEP(3, 2);
   else if (mt == 3 && ntt == 3) SEP(3, 3);
