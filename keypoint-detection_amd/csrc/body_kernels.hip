@@ -274,8 +274,8 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, cin_p = p.cin_p;
   float* es = sm;                                  // [Pin][ESTR]
-  float* wds = es + Pin * ESTR;                    // [K*K][CS]
-  float* ds = wds + K * K * CS;                    // [Po][CS] (pooled)
+  float* wds = es + Pin * ESTR;                    // [K*K][CS] depthwise weights, then [CS] its bias
+  float* ds = wds + (K * K + 1) * CS;              // [Po][CS] (pooled)
   float* w1s = ds + (p.pooled ? Po * CS : 0);      // [sq][CS] (part)
   const float* xg = p.x + (size_t)n * Pin * cin_p;
   stamp(p.stamps, 0);
@@ -290,6 +290,9 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
       bw[nt][kc] = *reinterpret_cast<const float4*>(p.we + (size_t)(c0 + nt * 16 + r) * cin_p + kc * 16 + g * 4);
+  float be[NTC];   // expand bias, loaded with the first round trip
+#pragma unroll
+  for (int nt = 0; nt < NTC; ++nt) be[nt] = p.be[c0 + nt * 16 + r];
   float4 av[DA][KC];
   auto load_a = [&](int t, float4* a4) {
     if (t < ntw) {
@@ -301,12 +304,14 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
   for (int d = 0; d < DA; ++d) load_a(d, av[d]);
   {
-    constexpr int NW = (K * K * CQ + 255) / 256;
+    // the depthwise weights and (row K*K) its bias
+    constexpr int NW = ((K * K + 1) * CQ + 255) / 256;
     float4 v[NW];
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
       const int i = tid + u * 256, t = i / CQ, q = i - t * CQ;
       if (i < K * K * CQ) v[u] = *reinterpret_cast<const float4*>(p.wd + (size_t)t * p.Ep + c0 + q * 4);
+      else if (i < (K * K + 1) * CQ) v[u] = *reinterpret_cast<const float4*>(p.bd + c0 + q * 4);
     }
     // the fc1 columns by LDS-DMA (no registers; waited for after the expand):
     // 16-byte piece e of w1s = [sq][CS] is w1[j][c0 + 4 q], e = j * CQ + q,
@@ -324,16 +329,13 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
       const int i = tid + u * 256;
-      if (i < K * K * CQ) reinterpret_cast<float4*>(wds)[i] = v[u];
+      if (i < (K * K + 1) * CQ) reinterpret_cast<float4*>(wds)[i] = v[u];
     }
   }
   stamp(p.stamps, 1);
   // expand: DA M tiles of A in flight per wave; a tile's slot is refilled
   // with the tile DA ahead right after its MFMAs
   {
-    float be[NTC];
-#pragma unroll
-    for (int nt = 0; nt < NTC; ++nt) be[nt] = p.be[c0 + nt * 16 + r];
     for (int t0 = 0; t0 < ntw; t0 += DA) {
 #pragma unroll
       for (int d = 0; d < DA; ++d) {
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
         }
       }
     }
-    const float4 b = *reinterpret_cast<const float4*>(p.bd + c0 + q * 4);
+    const float4 b = reinterpret_cast<const float4*>(wds)[K * K * CQ + q];
 #pragma unroll
     for (int o = 0; o < XT; ++o) {
       if (ox0 + o >= p.Wo) break;
@@ -1437,7 +1439,7 @@ size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
   // the fc1 columns are filled by 1 KiB LDS-DMA pieces: round up to whole pieces
   const size_t w1f = a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
-  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)K * K * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
+  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)(K * K + 1) * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
   return 4 * main;
 }
 
