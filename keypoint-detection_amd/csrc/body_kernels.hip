@@ -558,6 +558,20 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
     }
   }
   stamp(a.stamps, 2);
+  // the epilogue's bias and residual quads, loaded before the K loop (their
+  // latency hides under it instead of ending the workgroup)
+  constexpr int NQ = NT / 4, IT = (MP * NQ + NTH - 1) / NTH;
+  float4 ep_b[IT], ep_r[IT];
+  {
+    const float* res0 = a.res ? a.res + ((size_t)n * Po + m0) * a.cout_p + o0 : nullptr;
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int i = min(tid + u * NTH, Pr * NQ - 1), px = i / NQ, q = i - px * NQ;
+      ep_b[u] = *reinterpret_cast<const float4*>(a.bp + o0 + q * 4);
+      ep_r[u] = res0 ? *reinterpret_cast<const float4*>(res0 + (size_t)px * a.cout_p + q * 4)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   // (3) project on MFMA
   f32x4 acc[MT][NTT];
 #pragma unroll
@@ -598,10 +612,11 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
   __syncthreads();
   stamp(a.stamps, 3);
   // (4) sum the NWV waves in order, bias, residual; 4 channels per thread
-  constexpr int NQ = NT / 4;
   float* out = a.out + ((size_t)n * Po + m0) * a.cout_p + o0;
-  const float* res = a.res ? a.res + ((size_t)n * Po + m0) * a.cout_p + o0 : nullptr;
-  for (int i = tid; i < Pr * NQ; i += NTH) {
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = tid + u * NTH;
+    if (i >= Pr * NQ) break;
     const int px = i / NQ, q = i - px * NQ;
     float4 v = *reinterpret_cast<const float4*>(red + px * NT + q * 4);
 #pragma unroll
@@ -609,10 +624,10 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
       const float4 t = *reinterpret_cast<const float4*>(red + ((size_t)w * MP + px) * NT + q * 4);
       v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
     }
-    const float4 b = *reinterpret_cast<const float4*>(a.bp + o0 + q * 4);
+    const float4 b = ep_b[u];
     v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-    if (res) {
-      const float4 x = *reinterpret_cast<const float4*>(res + (size_t)px * a.cout_p + q * 4);
+    if (a.res) {
+      const float4 x = ep_r[u];
       v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
     }
     *reinterpret_cast<float4*>(out + (size_t)px * a.cout_p + q * 4) = v;

@@ -27,12 +27,11 @@ constexpr int FC = 128;             // FPN channels
 // ---------------------------------------------------------------- top-k
 // ChannelAttention + select_top_k_channels (keypoint_model.py:18-44,
 // 653-661).  One 256-thread workgroup per image.  stats: [N][tiles][2][128]
-// partial channel sums / maxima from the FPN level-0 epilogue.  The image's
-// partials and both FC weights are staged in LDS in one load round trip
-// (every load in flight before the first use); the sums then run in tile
-// order from LDS, as before.
+// partial channel sums / maxima from the FPN level-0 epilogue.  A thread
+// takes one (sum | max, channel) column of the partials, loads 48 tiles of it
+// into registers at once and reduces them in tile order; both FC weights go
+// to LDS in the same round trip.
 __device__ __forceinline__ void slotmap_image(const float* __restrict__ boxes, int b, int P, int32_t* __restrict__ slot);
-constexpr int kTopkMaxTiles = 144;   // LDS: tiles x 1 KB + 8 KB
 __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ stats, int tiles, int HW,
                                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                                    const float* __restrict__ w2, const float* __restrict__ b2,
@@ -40,48 +39,38 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sta
                                                    const float* __restrict__ boxes, int P, int32_t* __restrict__ slot,
                                                    float* __restrict__ imax, float* __restrict__ sc_zero, int sc_n) {
   extern __shared__ __attribute__((aligned(16))) float tsm[];
-  // more tiles than fit in LDS (the fp32 path's small tiles at 384x288):
-  // the partials are summed straight from global memory
-  const bool staged = tiles <= kTopkMaxTiles;
-  const int lt = staged ? tiles : 0;
-  float* sst = tsm;                        // [tiles][2][FC]
-  float* sw0 = sst + lt * 2 * FC;          // [8][FC]
+  float* sw0 = tsm;                        // [8][FC]
   float* sw2 = sw0 + 8 * FC;               // [FC][8]
   __shared__ float avg[FC], mx[FC], h[16], sc[FC];
   const int n = blockIdx.x, tid = threadIdx.x, c = tid;
   {
-    const float4* st4 = reinterpret_cast<const float4*>(stats + (size_t)n * tiles * 2 * FC);
-    const int nst = lt * 2 * FC / 4, nw = 8 * FC / 4, tot = nst + 2 * nw;
-    constexpr int U = 12;   // float4 per thread per pass (one pass up to 40 tiles)
-    for (int base = 0; base < tot; base += U * 256) {
-      float4 v[U];
+    // both FC weights -> LDS (2 float4 per thread), issued with the partials
+    float4 wv[2];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = base + tid + u * 256;
-        v[u] = i < nst ? st4[i]
-             : i < nst + nw ? reinterpret_cast<const float4*>(w0)[i - nst]
-             : i < tot ? reinterpret_cast<const float4*>(w2)[i - nst - nw] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 256;
+      wv[u] = i < 256 ? reinterpret_cast<const float4*>(w0)[i] : reinterpret_cast<const float4*>(w2)[i - 256];
+    }
+    // partials straight into registers: thread (kind = sum / max, channel)
+    // loads its column of every tile in batches of TB tiles, all in flight
+    // together (one round trip per batch instead of one per LDS staging pass),
+    // and reduces them in tile order as before
+    const int kind = tid >> 7, ch = tid & (FC - 1);
+    const float* col = stats + (size_t)n * tiles * 2 * FC + kind * FC + ch;
+    constexpr int TB = 48;
+    float acc = kind ? -INFINITY : 0.f;
+    for (int t0 = 0; t0 < tiles; t0 += TB) {
+      float v[TB];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = base + tid + u * 256;
-        if (i < tot) reinterpret_cast<float4*>(tsm)[i] = v[u];
-      }
+      for (int u = 0; u < TB; ++u) v[u] = col[(size_t)min(t0 + u, tiles - 1) * 2 * FC];
+#pragma unroll
+      for (int u = 0; u < TB; ++u)
+        if (t0 + u < tiles) acc = kind ? fmaxf(acc, v[u]) : acc + v[u];
     }
-  }
-  __syncthreads();
-  if (c < FC) {
-    const float* src = staged ? sst : stats + (size_t)n * tiles * 2 * FC;
-    float s = 0.f, m = -INFINITY;
-    // unrolled so the LDS reads of 16 tiles are in flight together (the adds
-    // stay in tile order)
-#pragma unroll 16
-    for (int t = 0; t < tiles; ++t) {
-      s += src[t * 2 * FC + c];
-      m = fmaxf(m, src[t * 2 * FC + FC + c]);
-    }
-    avg[c] = s / (float)HW;
-    mx[c] = m;
+    if (kind) mx[ch] = acc;
+    else avg[ch] = acc / (float)HW;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) reinterpret_cast<float4*>(tsm)[tid + u * 256] = wv[u];
   }
   __syncthreads();
   if (c < 16) {  // hidden units: 0..7 for avg branch, 8..15 for max branch
@@ -643,7 +632,7 @@ hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float
                        const float* w2, const float* b2, int32_t* topk, float* scores, hipStream_t st,
                        const float* boxes, int P, int32_t* slot, float* imax, float* sc_zero, int sc_n) {
   if (slot && (!boxes || P <= 0 || P > 0xFFFF)) return hipErrorInvalidValue;
-  const size_t lds = ((size_t)(tiles <= kTopkMaxTiles ? tiles : 0) * 2 * FC + 2 * 8 * FC) * 4;
+  const size_t lds = (size_t)2 * 8 * FC * 4;   // the two FC weights
   hipLaunchKernelGGL(topk_kernel, dim3(N), dim3(256), lds, st, stats, tiles, HW, w0, b0, w2, b2, topk, scores,
                      boxes, P, slot, imax, sc_zero, sc_n);
   return hipGetLastError();
