@@ -162,8 +162,14 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
                                                         const int32_t* __restrict__ topk,
                                                         const float* __restrict__ boxes, int P,
                                                         float* __restrict__ roi, float* __restrict__ roi_stats,
-                                                        int stage_cap) {
+                                                        int stage_cap, unsigned long long* __restrict__ stamps) {
   __shared__ float red[4][2][TOPK];
+  // diagnostic phase stamps (KPD_STAMPS): thread 0, s_memrealtime, row [8] per workgroup
+  auto stamp = [&](int i) {
+    if (stamps && threadIdx.x == 0)
+      stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   constexpr int CO = TOPK * CW;
   const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -267,6 +273,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
         }
       }
       __syncthreads();
+      if (iy == 0) stamp(1);
       for (int ix = 0; ix < gw; ++ix) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
@@ -325,6 +332,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     }
   }
   }
+  stamp(2);
   float s_sum = 0.f, s_max = -INFINITY;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -348,6 +356,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     st[lane] = s;
     st[TOPK + lane] = m;
   }
+  stamp(3);
 }
 
 // ---------------------------------------------------------------- HeatmapHead channel attention
@@ -643,7 +652,7 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot, hipSt
   return hipGetLastError();
 }
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk, const float* boxes,
-                            int R, int P, float* roi, float* roi_stats, hipStream_t st) {
+                            int R, int P, float* roi, float* roi_stats, hipStream_t st, unsigned long long* stamps) {
   // the stage holds at most the map's width of interpolated columns: sized to
   // that (64 channels at Wf 96: 24 KB, 6 workgroups per CU instead of 3)
   static const bool full_cap = getenv("KPD_ROI_FULLCAP") != nullptr;   // A/B: the fixed 50 KB stage
@@ -651,13 +660,13 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
     static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
     const int cap = direct ? 0 : full_cap ? kRoiStageFloats : std::min(kRoiStageFloats, Wf * TOPK);
     hipLaunchKernelGGL((roi_align_kernel<1>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, topk, boxes, P,
-                       roi, roi_stats, cap);
+                       roi, roi_stats, cap, stamps);
   } else {
     if (Cf != 2 * TOPK) return hipErrorInvalidValue;
     static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
     const int cap = direct ? 0 : full_cap ? kRoiStageFloats : std::min(kRoiStageFloats, Wf * 2 * TOPK);
     hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
-                       roi, nullptr, cap);
+                       roi, nullptr, cap, stamps);
   }
   return hipGetLastError();
 }

@@ -281,7 +281,7 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
                             const float* boxes, int R, int P, float* roi, float* roi_stats,
-                            hipStream_t st);
+                            hipStream_t st, unsigned long long* stamps = nullptr);   // stamps: KPD_STAMPS [grid][8]
 // hsc != null (split heatmap convs): writes hsc[r][0] = max of ROI r's
 // features (the bound of |xs|: the model's ROI features follow a ReLU) and
 // zeroes hsc[r][1]; abs_in = 1: the features may be negative, hsc[r][2]

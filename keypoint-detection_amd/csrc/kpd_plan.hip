@@ -1696,7 +1696,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   {
     Stage sg(p, "roi_align", st);
     if (!slot_in_topk) HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
-    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st));
+    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st,
+                             take_stamps("stamps_roi_0", (size_t)56 * R)));
   }
   if (int rc = mark(5)) return rc;
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
