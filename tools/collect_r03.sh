@@ -9,6 +9,10 @@ cp $F/smoke.log $D/smoke.log
 tail -1 $F/bench_driver_cmd.json > $D/bench_driver_cmd.json
 tail -1 $F/bench_default.json > $D/bench_default.json
 cp $F/configs.jsonl $D/configs_c1_c3_c5.jsonl
+for C in c3 c5; do
+  U=$(echo $C | tr a-z A-Z)
+  if [ -f gpurun_out/c35/prof_$U/run_kernel_stats.csv ]; then cp gpurun_out/c35/prof_$U/run_kernel_stats.csv $D/kernel_stats_$C.csv; fi
+done
 cp $P/trace/run_kernel_stats.csv $D/kernel_stats_driver_cmd.csv
 cp $P/stages.json $D/stages_driver_cmd.json
 grep -o '{"metric.*' $P/trace.log > $D/bench_driver_cmd_under_rocprof.json

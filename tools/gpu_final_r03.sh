@@ -26,3 +26,6 @@ python3 -c "
 import json
 for l in open('$OUT/configs.jsonl'):
     d = json.loads(l); print(d['config'], d.get('images_per_s', d.get('gpu_latency_ms')), (d.get('roofline') or {}).get('frac'))"
+# kernel traces of C3 and C5 alone (profiles/r03/kernel_stats_c3.csv, _c5.csv)
+SKIP_CFG=1 bash tools/gpu_c35prof.sh > "$OUT/c35prof.txt" 2>&1 || { echo "c35prof failed"; tail -5 "$OUT/c35prof.txt"; exit 1; }
+echo "c35 kernel traces ok"
