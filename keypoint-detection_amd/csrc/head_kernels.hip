@@ -530,6 +530,123 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- spatial pool + apply, fused
+// hm_spool_kernel and hm_sapply_kernel in one launch: a 512-thread workgroup
+// takes a band of BR = 8 rows of one ROI.  (A) its waves pool the band's rows
+// and the 3-row halo on either side (mean and max over channels of roi * cw,
+// as hm_spool_kernel: same lane layout and reduction order) into LDS;
+// (B) sw for the band's pixels (the 7x7 conv, same tap order as
+// hm_sapply_kernel); (C) one wave per band row re-reads that row (the same
+// workgroup read it in (A): an L2 hit) and applies cw * sw with the same
+// output modes.  The map never reaches HBM and the ROI features leave HBM
+// once.  Bands of one ROI are consecutive logical workgroups and a ROI's
+// bands share an XCD (xcd-contiguous order; every ROI is the same work), so
+// the halo rows a neighbour band re-reads are L2 hits.
+constexpr int kAttBR = 8;
+__global__ __launch_bounds__(512) void hm_attn_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
+                                                      const float* __restrict__ saw, const float* __restrict__ sab,
+                                                      void* __restrict__ xs, int out_bf16, const float* __restrict__ hsc,
+                                                      int use_sp, float* __restrict__ sw_out) {
+  constexpr int NI = HM / 4, BR = kAttBR, PR = BR + 6;
+  __shared__ float w[98];
+  __shared__ float2 pool[PR][HM + 6];   // pooled rows y0 - 3 .. y0 + BR + 2, zero-padded by 3 columns
+  __shared__ float ssw[BR][HM];
+  const int nb = HM / BR;
+  const int nblk = gridDim.x, L = blockIdx.x;
+  // xcd-contiguous logical order (dispatch round-robins the 8 XCDs)
+  const int qx = nblk / 8, rx = nblk % 8, x8 = L % 8, k8 = L / 8;
+  const int g = (x8 < rx ? x8 * (qx + 1) : rx * (qx + 1) + (x8 - rx) * qx) + k8;
+  const int r = g / nb, y0 = (g - r * nb) * BR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pp = lane >> 4, c = lane & 15;
+  const float4 cq = reinterpret_cast<const float4*>(cw + (size_t)r * TOPK)[c];
+  if (tid < 98) w[tid] = saw[tid];
+  // zero padding columns of the pooled rows
+  for (int i = tid; i < PR * 6; i += 512) {
+    const int rr = i / 6, cc = i - rr * 6;
+    pool[rr][cc < 3 ? cc : HM + cc] = make_float2(0.f, 0.f);
+  }
+  // (A) pooled rows: wave w takes rows y0 - 3 + w and + 8 (zero outside the ROI)
+  for (int pr = wave; pr < PR; pr += 8) {
+    const int y = y0 - 3 + pr;
+    if (y < 0 || y >= HM) {
+      if (lane < HM) pool[pr][lane + 3] = make_float2(0.f, 0.f);
+      continue;
+    }
+    const float4* src = reinterpret_cast<const float4*>(roi + ((size_t)r * HM + y) * HM * TOPK);
+    float4 v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) v[i] = src[(4 * i + pp) * (TOPK / 4) + c];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const float a = v[i].x * cq.x, b = v[i].y * cq.y, cc = v[i].z * cq.z, d = v[i].w * cq.w;
+      float sm = (a + b) + (cc + d), m = fmaxf(fmaxf(a, b), fmaxf(cc, d));
+      sm += dpp_f<0xB1>(sm); m = fmaxf(m, dpp_f<0xB1>(m));
+      sm += dpp_f<0x4E>(sm); m = fmaxf(m, dpp_f<0x4E>(m));
+      sm += dpp_f<0x124>(sm); m = fmaxf(m, dpp_f<0x124>(m));
+      sm += dpp_f<0x128>(sm); m = fmaxf(m, dpp_f<0x128>(m));
+      if (c == 0) pool[pr][4 * i + pp + 3] = make_float2(sm / (float)TOPK, m);
+    }
+  }
+  __syncthreads();
+  // (B) sw of the band's pixels
+  if (tid < BR * HM) {
+    const int j = tid / HM, x = tid - j * HM, y = y0 + j;
+    float a = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      const int iy = y + ky - 3;
+      if (iy < 0 || iy >= HM) continue;
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) {
+        const int ix = x + kx - 3;
+        if (ix < 0 || ix >= HM) continue;
+        const float2 sv2 = pool[j + ky][x + kx];
+        a = fmaf(w[ky * 7 + kx], sv2.x, a);
+        a = fmaf(w[49 + ky * 7 + kx], sv2.y, a);
+      }
+    }
+    ssw[j][x] = use_sp ? kpd_sigmoid(a + sab[0]) : 1.f;
+    if (sw_out) sw_out[((size_t)r * HM + y) * HM + x] = ssw[j][x];
+  }
+  const float ssc = out_bf16 == 3 ? ldexpf(1.f, split_exp_of(hsc[(size_t)r * 4])) : 1.f;
+  __syncthreads();
+  // (C) band row wave: roi * cw * sw -> the first heatmap conv's operand
+  {
+    const int j = wave, y = y0 + j;
+    const float4* src = reinterpret_cast<const float4*>(roi + ((size_t)r * HM + y) * HM * TOPK);
+    float4 v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) v[i] = src[(4 * i + pp) * (TOPK / 4) + c];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int px = 4 * i + pp;
+      const float sw = ssw[j][px];
+      const float4 o = make_float4((v[i].x * cq.x) * sw, (v[i].y * cq.y) * sw, (v[i].z * cq.z) * sw, (v[i].w * cq.w) * sw);
+      if (out_bf16 == 3) {
+        const size_t opix = ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1;
+        const float ov[4] = {o.x * ssc, o.y * ssc, o.z * ssc, o.w * ssc};
+        f16x4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hi[e] = (_Float16)ov[e];
+          lo[e] = (_Float16)(ov[e] - (float)hi[e]);
+        }
+        _Float16* ob = reinterpret_cast<_Float16*>(xs) + opix * 2 * TOPK + (c >> 3) * 64 + (c & 7) * 4;
+        *reinterpret_cast<f16x4*>(ob) = hi;
+        *reinterpret_cast<f16x4*>(ob + 32) = lo;
+      } else if (out_bf16) {
+        const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1
+                                          : ((size_t)r * HM + y) * HM + px;
+        bf16x4 ob;
+        ob[0] = (__bf16)o.x; ob[1] = (__bf16)o.y; ob[2] = (__bf16)o.z; ob[3] = (__bf16)o.w;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(xs) + opix * TOPK + 4 * c) = ob;
+      } else {
+        reinterpret_cast<float4*>(reinterpret_cast<float*>(xs) + (((size_t)r * HM + y) * HM + px) * TOPK)[c] = o;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- final 1x1 + sigmoid
 // grid (56 rows, R), 64 threads (pixel x).  h3: [R][3136][64] f32.
 // heat_out: [B][P][17][56][56] written at the box's compacted slot.
@@ -684,6 +801,14 @@ hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap
                             int use_sp, float* sw_out) {
   hipLaunchKernelGGL(hm_sapply_kernel, dim3(HM, R), dim3(64), 0, st, roi, cw, smap, saw, sab, xs, out_bf16, hsc,
                      use_sp, sw_out);
+  return hipGetLastError();
+}
+hipError_t launch_hm_attn(const float* roi, const float* cw, const float* saw, const float* sab, int R, void* xs,
+                          int out_bf16, hipStream_t st, const float* hsc, int use_sp, float* sw_out) {
+  static_assert(HM % kAttBR == 0 && kAttBR == 8, "one wave per band row");
+  if (R <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hm_attn_kernel, dim3((unsigned)(R * (HM / kAttBR))), dim3(512), 0, st, roi, cw, saw, sab, xs,
+                     out_bf16, hsc, use_sp, sw_out);
   return hipGetLastError();
 }
 hipError_t launch_hm_final(const float* h3, int R, const float* w, const float* b, const int32_t* slot, int P,

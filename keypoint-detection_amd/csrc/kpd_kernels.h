@@ -292,6 +292,9 @@ hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, cons
 hipError_t launch_hm_spool(const float* roi, const float* cw, int R, float* smap, hipStream_t st);
 // use_sp = 0: no spatial attention (weights 1); sw_out != null: the spatial
 // weights [R][56][56] (HeatmapHead.forward's attention_weights[1])
+// hm_spool + hm_sapply in one launch (bands of 8 rows; no pooled map in HBM)
+hipError_t launch_hm_attn(const float* roi, const float* cw, const float* saw, const float* sab, int R, void* xs,
+                          int out_bf16, hipStream_t st, const float* hsc, int use_sp, float* sw_out);
 hipError_t launch_hm_sapply(const float* roi, const float* cw, const float* smap, const float* saw,
                             const float* sab, int R, void* xs, int out_bf16, hipStream_t st,
                             const float* hsc = nullptr, int use_sp = 1, float* sw_out = nullptr);

@@ -1243,11 +1243,17 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
   HIP_TRY(launch_hm_chattn(w.roi_stats, R, p->hca_w0, p->hca_b0, p->hca_w2, p->hca_b2, w.cw,
                            hsplit ? w.hsc : nullptr, st, abs_in));
   if (!(parts & KPD_HEAD_CHANNEL_ATT)) HIP_TRY(launch_fill(w.cw, (long)R * 64, 1.f, st));
-  HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
   const bool bf = p->precision == KPD_PRECISION_MIXED;
   const int xs_mode = hsplit ? 3 : bf ? (hm_padded(p) ? 2 : 1) : 0;
-  HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc,
+  static const bool att_2k = getenv("KPD_HM_ATT_2K") != nullptr;   // A/B: pool and apply as two launches
+  if (att_2k) {
+    HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
+    HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc,
+                             (parts & KPD_HEAD_SPATIAL_ATT) != 0, sw_out));
+  } else {
+    HIP_TRY(launch_hm_attn(w.roi, w.cw, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc,
                            (parts & KPD_HEAD_SPATIAL_ATT) != 0, sw_out));
+  }
   att_stage.reset();
   if (!(parts & KPD_HEAD_CONVS)) return KPD_OK;
   // bounds: |xs| <= U0; |h1| <= bc1 + bs1 U0; |h2| <= bc2 + bs2 max|h1| (the
