@@ -26,7 +26,7 @@ constexpr int kSeExcitePart = 6144;   // fc1 partial floats per image staged by 
 // of a buffer no other code reads.
 __device__ __forceinline__ void stamp(unsigned long long* st, int i) {
   if (st && threadIdx.x == 0)
-    st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+    st[(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Stem: 3x3 stride-2 conv (CIN -> 16) + folded BN + h-swish, NCHW image in,
@@ -272,12 +272,18 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
   constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = CS + 4, DA = KC <= 3 ? 4 : 1;
   const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Pin = p.Hi * p.Wi, Po = p.Ho * p.Wo, cin_p = p.cin_p;
+  constexpr int PD = (K - 1) / 2;
+  // row band (blockIdx.z of gridDim.z; no SE): output rows [oy0, oy1), from
+  // input rows [iy_lo, iy_hi) -- the depthwise halo rows are expanded by both
+  // neighbouring bands
+  const int oy0 = blockIdx.z * p.Ho / gridDim.z, oy1 = (blockIdx.z + 1) * p.Ho / gridDim.z;
+  const int iy_lo = max(0, oy0 * S - PD), iy_hi = min(p.Hi, (oy1 - 1) * S - PD + K);
+  const int Pin = (iy_hi - iy_lo) * p.Wi, Po = p.Ho * p.Wo, cin_p = p.cin_p;
   float* es = sm;                                  // [Pin][ESTR]
   float* wds = es + Pin * ESTR;                    // [K*K][CS] depthwise weights, then [CS] its bias
   float* ds = wds + (K * K + 1) * CS;              // [Po][CS] (pooled)
   float* w1s = ds + (p.pooled ? Po * CS : 0);      // [sq][CS] (part)
-  const float* xg = p.x + (size_t)n * Pin * cin_p;
+  const float* xg = p.x + ((size_t)n * p.Hi + iy_lo) * p.Wi * cin_p;
   stamp(p.stamps, 0);
   const int r = lane & 15, g = lane >> 4;
   const int nmt = (Pin + 15) / 16, ntw = (nmt - wave + 3) / 4;   // M tiles of this wave: wave + 4 t
@@ -372,10 +378,10 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   stamp(p.stamps, 2);
   // depthwise from LDS, XT consecutive output columns per thread (input
   // columns reused from registers as in dwconv_kernel)
-  constexpr int PD = (K - 1) / 2, NC = (XT - 1) * S + K;
+  constexpr int NC = (XT - 1) * S + K;
   const int wx = (p.Wo + XT - 1) / XT;
-  for (int i = tid; i < p.Ho * wx * CQ; i += 256) {
-    const int q = i % CQ, rr = i / CQ, xt = rr % wx, oy = rr / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
+  for (int i = tid; i < (oy1 - oy0) * wx * CQ; i += 256) {
+    const int q = i % CQ, rr = i / CQ, xt = rr % wx, oy = oy0 + rr / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
     float4 a[XT];
 #pragma unroll
     for (int o = 0; o < XT; ++o) a[o] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -387,7 +393,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int ix = ix0 + c;
-        col[c] = (ix >= 0 && ix < p.Wi) ? *reinterpret_cast<const float4*>(es + (iy * p.Wi + ix) * ESTR + q * 4)
+        col[c] = (ix >= 0 && ix < p.Wi) ? *reinterpret_cast<const float4*>(es + ((iy - iy_lo) * p.Wi + ix) * ESTR + q * 4)
                                          : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
@@ -1451,7 +1457,9 @@ hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st) {
 }
 
 size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
-  const int Pin = a.Hi * a.Wi, Po = a.Ho * a.Wo;
+  // a band's input rows: at most ceil(Ho / nband) output rows' worth
+  const int nb = a.nband > 1 ? a.nband : 1, S = a.Hi > a.Ho ? 2 : 1;
+  const int Pin = std::min(a.Hi, ((a.Ho + nb - 1) / nb - 1) * S + K) * a.Wi, Po = a.Ho * a.Wo;
   // the fc1 columns are filled by 1 KiB LDS-DMA pieces: round up to whole pieces
   const size_t w1f = a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
   const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)(K * K + 1) * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
@@ -1462,11 +1470,12 @@ hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
   const int kc = a.cin_p / 16;
   if ((a.CS != 16 && a.CS != 32 && a.CS != 48) || a.Ep % a.CS || a.cin_p % 16 || (kc != 2 && kc != 3 && kc != 6) ||
       !a.we ||
-      (a.part && (!a.pooled || !a.w1 || a.sq <= 0 || a.sq > 144 || a.C % 4)))
+      (a.part && (!a.pooled || !a.w1 || a.sq <= 0 || a.sq > 144 || a.C % 4)) ||
+      (a.nband > 1 && (a.pooled || a.part || a.nband > a.Ho)))
     return hipErrorInvalidValue;
   const size_t lds = exdw_lds_bytes(a, K);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(a.Ep / a.CS, N);
+  const dim3 grid(a.Ep / a.CS, N, a.nband > 1 ? a.nband : 1);
   const bool xt4 = a.Wo >= 12;
 #define EXDW_KC(KK, SS, NTC, XT)                                                                        \
   do {                                                                                                  \

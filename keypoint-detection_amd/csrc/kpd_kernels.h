@@ -178,6 +178,7 @@ struct ExDwArgs {
   float* part;           // optional [N][Ep/CS][sq] fc1 partial products (needs pooled)
   int sq, C;
   unsigned long long* stamps;   // diagnostic phase stamps, [grid][8] (KPD_STAMPS), normally null
+  int nband;             // > 1 (no SE only): output rows split over nband workgroups per (image, slice)
 };
 size_t exdw_lds_bytes(const ExDwArgs& a, int K);
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st);

@@ -1506,6 +1506,11 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       // 32 channels from 288 expanded channels up, else 16 (48 for the
       // 576-wide blocks measured slower: 188 VGPRs, 30 vs 23 us)
       xa.CS = cs_env > 0 ? cs_env : (bn.dw.Cp >= 288 ? 32 : 16);
+      // no SE and under two workgroups per CU: split the output rows in two
+      // bands (features.3 at 64 images: 384 -> 768 workgroups)
+      static const int nband_env = getenv("KPD_EXDW_NBAND") ? atoi(getenv("KPD_EXDW_NBAND")) : 0;   // A/B
+      xa.nband = !bn.cfg.se && (long)(bn.dw.Cp / xa.CS) * B < 512 ? 2 : 1;
+      if (nband_env > 0 && !bn.cfg.se) xa.nband = std::min(nband_env, ho);
       fused = bn.dw.Cp % xa.CS == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 160 * 1024;
     }
     // SE blocks on the coarse maps: fc1 partials in exdw_kernel, then the
@@ -1518,7 +1523,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       if (seproj) {
         xa.part = w.separt; xa.w1 = bn.se.w1; xa.sq = bn.se.sq; xa.C = bn.se.C;
       }
-      xa.stamps = take_stamps("stamps_exdw_" + std::to_string(i), (size_t)(bn.dw.Cp / xa.CS) * B);
+      xa.stamps = take_stamps("stamps_exdw_" + std::to_string(i), (size_t)(bn.dw.Cp / xa.CS) * B * std::max(1, xa.nband));
       HIP_TRY(launch_exdw(xa, B, bn.dw.k, bn.dw.s, st));
     }
     if (seproj) {
@@ -1540,7 +1545,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
         HIP_TRY(launch_se_excite(sa, B, w.sesc[i], st));
         sa.sesc = w.sesc[i];
       }
-      sa.stamps = take_stamps("stamps_seproj_" + std::to_string(i), (size_t)(sa.cout_p / sa.NT) * B);
+      sa.stamps = take_stamps("stamps_seproj_" + std::to_string(i), (size_t)(sa.cout_p / sa.NT) * B * 2);   // (x msplit)
       HIP_TRY(launch_seproj(sa, B, st));
       x = w.o[i];
       if (i + 1 == 3) taps[1] = x;

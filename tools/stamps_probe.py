@@ -42,6 +42,9 @@ def main():
         except Exception:
             continue
         st = buf.view(torch.int64).cpu().numpy().reshape(-1, 8)
+        st = st[(st != 0).any(axis=1)]   # rows of workgroups this launch did not have (sized for the largest grid)
+        if len(st) == 0:
+            continue
         used = [c for c in range(8) if (st[:, c] != 0).all()]
         t = st[:, used].astype(np.float64) * 10.0 / 1000.0   # us
         t0 = t[:, 0].min()
