@@ -133,6 +133,27 @@ def test_odd_size_vs_oracle(model_sd, precision):
         np.testing.assert_allclose(out["heatmap"].cpu().numpy(), ref["heatmap"].numpy(), atol=3e-2)
 
 
+@pytest.mark.parametrize("precision", ["split"])
+def test_large_map_lateral_fallback(model_sd, precision):
+    """480x384: lateral 3 is 15 x 12 = 180 pixels, more than the fused lateral
+    chain takes (lateral_chain_ok: <= 128), so the split path runs the
+    per-level lateral convs and split_rows for lateral 1 and the stem tap (the
+    max-based scale, not the chain's bound)."""
+    from dll.models.synthetic import synthetic_images
+    img = synthetic_images(1, 3, 480, 384, seed=9)
+    boxes = torch.tensor([[[0.45, 0.55, 0.4, 0.7]]])
+    ref = O.forward(model_sd, {"image": img, "bboxes": boxes}, return_debug=True)
+    m = _model(model_sd, precision)
+    with torch.no_grad():
+        out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
+    plan = m.native_plan(DEV)
+    f = _nchw_feat(plan, 1, 240, 192)
+    np.testing.assert_allclose(f.numpy(), ref["_feat0"].numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
+    np.testing.assert_allclose(out["heatmap"].cpu().numpy(), ref["heatmap"].numpy(), atol=5e-5)
+
+
 def test_roi_features_vs_oracle(model_sd):
     from dll.models.synthetic import synthetic_boxes, synthetic_images
     img = synthetic_images(2, 3, 256, 192, seed=21)
