@@ -38,14 +38,17 @@ def label(forward):
     """Stage label per dispatch of one forward (list of kernel names)."""
     out, hm = [], 0
     for k in forward:
+        targs = [t.strip() for t in k[len("hmconv_kernel<"):].split(">")[0].split(",")] \
+            if k.startswith("hmconv_kernel<") else []
         if k.startswith("fpn0x_kernel"):
             out.append("fpn0")
+        elif len(targs) >= 10 and targs[9] == "2":
+            out.append("kh_conv")   # KEYPOINT_HEAD convs (MODE 2), dual-head configs
         elif k.startswith("hmconv_kernel<64"):
             out.append("hm_conv3")
         elif k.startswith("hmconv_kernel<"):
             # conv 1 / conv 2 by the compile-time input channels (6th template
             # argument: 64 / 256; a conv may be two launches), else by order
-            targs = [t.strip() for t in k[len("hmconv_kernel<"):].split(">")[0].split(",")]
             hm += 1
             if len(targs) >= 6 and targs[5] in ("64", "256"):
                 out.append("hm_conv1" if targs[5] == "64" else "hm_conv2")
