@@ -183,6 +183,19 @@ int kpd_adaptive_heatmap_loss(const float* pred, const float* gt, const float* t
  * on n: every split-precision scale is per image / per ROI. */
 int kpd_plan_set_streams(kpd_plan* plan, int n);
 
+/* Not part of the reference interface: replay whole forwards as hipGraphs.
+ * With enable != 0, a kpd_forward call whose signature (shapes, flags, every
+ * buffer address, the stream) repeats runs eagerly once, is captured the
+ * second time and from then on is one hipGraphLaunch on the caller's stream
+ * (the ~60 launches of a forward, not its kernels, set the latency of a
+ * small batch).  A workspace re-carve or re-finalize invalidates the graphs;
+ * stage timing forces eager forwards.  Results are identical either way.
+ * Default: off (KPD_GRAPH=1 in the environment: on).  Measured at 64 and 1
+ * images back to back, replay is no faster than the eager launches (the GPU
+ * is the bound there); one synchronous 1-image forward (C1) took 0.62 ms
+ * replayed against 0.67 ms eager. */
+int kpd_plan_set_graphs(kpd_plan* plan, int enable);
+
 /* Diagnostics (not part of the reference interface): times the LDS-DMA 3x3
  * conv (conv_glds.hip) on synthetic operands, N x H x W pixels, cin -> cout;
  * split != 0 selects the fp32-accurate FPN level-0 form (cin = cout = 128).

@@ -236,6 +236,15 @@ struct kpd_plan {
   // passes a stage mark, so its latency-bound body overlaps k's heavy stages
   hipEvent_t pipe_ev[kMaxSub] = {};
   bool keep_laterals = false;   // kpd_backbone: every lateral level is an output (no fused chain)
+  // hipGraph replay of whole forwards (KPD_GRAPH=1): one executable graph per
+  // call signature (shapes, flags, every buffer address, stream), valid while
+  // the workspace carve and the weights are the ones it was captured on
+  struct GraphEntry { hipGraphExec_t exec = nullptr; long epoch = -1; int seen = 0; };
+  std::map<std::vector<uintptr_t>, GraphEntry> graphs;
+  long ws_epoch = 0;             // bumped whenever a workspace is re-carved or the weights re-packed
+  bool use_graphs = getenv("KPD_GRAPH") != nullptr && atoi(getenv("KPD_GRAPH")) != 0;   // kpd_plan_set_graphs (KPD_GRAPH=1: on)
+  hipStream_t graph_st = nullptr;   // capture stream (the caller's may be the legacy default stream)
+  hipEvent_t graph_ev = nullptr;
   hipStream_t sub_st_pri[kMaxSub] = {};   // high-priority sub-batch streams (KPD_PIPE_PRI)
   std::map<std::string, std::pair<const void*, size_t>> debug;
   unsigned long long* stamps = nullptr;   // KPD_STAMPS diagnostic buffer (kStampWords)
@@ -893,6 +902,10 @@ void kpd_plan_destroy(kpd_plan* p) {
     if (p->pipe_ev[k]) (void)hipEventDestroy(p->pipe_ev[k]);
   }
   if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
+  for (auto& kv : p->graphs)
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  if (p->graph_st) (void)hipStreamDestroy(p->graph_st);
+  if (p->graph_ev) (void)hipEventDestroy(p->graph_ev);
   for (auto& kv : p->timers)
     for (auto& e : kv.second.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   (void)hipSetDevice(cur);
@@ -1143,6 +1156,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     return fail(KPD_EINVAL, "heatmap head channel chain mismatch");
   if (p->has_body && p->bn[0].cfg.cin != 16) return fail(KPD_EINVAL, "bad body");
   p->finalized = true;
+  ++p->ws_epoch;
   return KPD_OK;
 }
 
@@ -1179,6 +1193,7 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   }
   carve(p, d, reinterpret_cast<char*>(p->ws[k]), p->work[k]);
   p->work[k].sc_dirty = true;
+  ++p->ws_epoch;   // captured graphs hold the old carve's addresses
   // zero once: the padded heatmap-conv maps keep their zero border (the
   // kernels write interiors only)
   if (hm_padded(p)) HIP_TRY(hipMemsetAsync(p->ws[k], 0, need, st));
@@ -1730,9 +1745,87 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   return KPD_OK;
 }
 
+static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
+                        int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis,
+                        float* box_scores, int32_t* topk_out, void* stream);
+
+// KPD_GRAPH=1: a forward is a launch-bound chain of ~60 kernels (at one image
+// the launches, not the kernels, set the latency), so a repeated call with the
+// same signature replays one captured hipGraph.  The first call of a
+// signature runs eagerly (it may allocate the workspace); the second is
+// captured on the plan's own stream (the caller's may be the legacy default
+// stream, which cannot capture) and launched on the caller's; later calls
+// only launch.  Stage timing and debug buffers need eager forwards: graphs
+// are off while timing is on.
 int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
                 int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis, float* box_scores,
                 int32_t* topk_out, void* stream) {
+  if (!p || !p->use_graphs || !p->finalized || p->timing)
+    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
+                        topk_out, stream);
+  const std::vector<uintptr_t> key = {
+      (uintptr_t)image, (uintptr_t)B, (uintptr_t)C, (uintptr_t)H, (uintptr_t)W, (uintptr_t)boxes, (uintptr_t)NB,
+      (uintptr_t)P, (uintptr_t)flags, (uintptr_t)kpts, (uintptr_t)vis, (uintptr_t)heat, (uintptr_t)kh_kpts,
+      (uintptr_t)kh_vis, (uintptr_t)box_scores, (uintptr_t)topk_out, (uintptr_t)stream, (uintptr_t)p->streams};
+  if (p->graphs.size() >= 64 && !p->graphs.count(key)) {   // signatures that never repeat: bounded
+    for (auto& kv : p->graphs)
+      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    p->graphs.clear();
+  }
+  kpd_plan::GraphEntry& g = p->graphs[key];
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (g.exec && g.epoch == p->ws_epoch) {
+    HIP_TRY(hipSetDevice(p->device));
+    // the graph assumes zeroed split-scale slots (each forward's top-k kernel
+    // re-zeroes the ones it used); a forward without top-k in between
+    // (kpd_backbone) leaves them set: zero them here, as an eager forward would
+    for (int k = 0; k <= kpd_plan::kMaxSub; ++k)
+      if (p->have_work[k] && p->work[k].sc_dirty) {
+        HIP_TRY(hipMemsetAsync(p->work[k].sc, 0, (size_t)2 * p->dims[k].B * kAmaxStride * sizeof(float), st));
+        p->work[k].sc_dirty = false;
+      }
+    HIP_TRY(hipGraphLaunch(g.exec, st));
+    return KPD_OK;
+  }
+  if (g.exec) {
+    (void)hipGraphExecDestroy(g.exec);
+    g.exec = nullptr;
+    g.seen = 0;
+  }
+  if (g.seen++ == 0)   // eager: allocations and first-use setup happen outside any capture
+    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
+                        topk_out, stream);
+  HIP_TRY(hipSetDevice(p->device));
+  if (!p->graph_st) HIP_TRY(hipStreamCreateWithFlags(&p->graph_st, hipStreamNonBlocking));
+  if (!p->graph_ev) HIP_TRY(hipEventCreateWithFlags(&p->graph_ev, hipEventDisableTiming));
+  const long epoch0 = p->ws_epoch;
+  HIP_TRY(hipStreamBeginCapture(p->graph_st, hipStreamCaptureModeRelaxed));
+  const int rc = forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis,
+                              box_scores, topk_out, p->graph_st);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(p->graph_st, &graph);
+  if (rc != KPD_OK || ec != hipSuccess || p->ws_epoch != epoch0) {
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipGetLastError();
+    // not capturable here (an allocation or sync inside it, the carve changed
+    // under it): this call runs eagerly and reports its own errors
+    g.seen = 0;
+    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
+                        topk_out, stream);
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  HIP_TRY(ei);
+  g.exec = exec;
+  g.epoch = p->ws_epoch;
+  HIP_TRY(hipGraphLaunch(g.exec, st));
+  return KPD_OK;
+}
+
+static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,
+                        int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis,
+                        float* box_scores, int32_t* topk_out, void* stream) {
   if (!p) return fail(KPD_EINVAL, "null plan");
   if (!p->finalized) return fail(KPD_ESTATE, "plan not finalized");
   if (!p->has_body || !p->has_fpn || !p->has_ca || !p->has_hm)
@@ -1821,12 +1914,19 @@ int kpd_plan_set_streams(kpd_plan* p, int n) {
   return KPD_OK;
 }
 
+int kpd_plan_set_graphs(kpd_plan* p, int enable) {
+  if (!p) return fail(KPD_EINVAL, "null plan");
+  p->use_graphs = enable != 0;
+  return KPD_OK;
+}
+
 int kpd_plan_set_detector(kpd_plan* p, float conf_threshold, float nms_iou_threshold) {
   if (!p) return fail(KPD_EINVAL, "null plan");
   if (!(conf_threshold >= 0.f && conf_threshold <= 1.f) || !(nms_iou_threshold >= 0.f && nms_iou_threshold <= 1.f))
     return fail(KPD_EINVAL, "thresholds must be in [0, 1]");
   p->det_conf = conf_threshold;
   p->det_iou = nms_iou_threshold;
+  ++p->ws_epoch;   // captured forwards hold the old thresholds
   return KPD_OK;
 }
 

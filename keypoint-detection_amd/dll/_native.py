@@ -32,7 +32,7 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
            "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
            "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss", "kpd_conv3x3_forward",
-           "kpd_conv3x3_backward")
+           "kpd_conv3x3_backward", "kpd_plan_set_graphs")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 HEAD_CHANNEL_ATT, HEAD_SPATIAL_ATT, HEAD_CONVS, HEAD_ALL = 1, 2, 4, 7
@@ -159,6 +159,10 @@ class Plan:
     def set_streams(self, n: int) -> None:
         """Sub-batch streams for large batches (kpd_plan_set_streams)."""
         check(self.lib.kpd_plan_set_streams(self.h, int(n)), "kpd_plan_set_streams")
+
+    def set_graphs(self, enable: bool) -> None:
+        """Replay repeated forwards as hipGraphs (kpd_plan_set_graphs)."""
+        check(self.lib.kpd_plan_set_graphs(self.h, 1 if enable else 0), "kpd_plan_set_graphs")
 
     def forward(self, image: torch.Tensor, boxes: Optional[torch.Tensor], kpts, vis, heat, flags: int = 0,
                 kh_kpts=None, kh_vis=None, box_scores=None, topk=None) -> None:

@@ -329,6 +329,46 @@ def test_sub_batch_streams_match(model_sd, precision):
     assert torch.equal(a["visibilities"], b["visibilities"])
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_graph_replay_matches_eager(model_sd, streams):
+    """kpd_plan_set_graphs: the same call signature runs eagerly, is captured,
+    then replays one hipGraph per call -- outputs bit-identical to the eager
+    forward at every call, also with new inputs copied into the same buffers
+    and with sub-batch streams inside the graph."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m = _model(model_sd, "split")
+    m.streams = streams
+    B, P = 32, 2
+    img = synthetic_images(B, 3, 256, 192, seed=81, device=DEV)
+    boxes = synthetic_boxes(B, P, seed=82, device=DEV)
+    with torch.no_grad():
+        ref = m({"image": img, "bboxes": boxes})           # eager: the plan is built here
+    plan = m.native_plan(DEV)
+    kpts = torch.empty(B, P, 1, 17, 2, device=DEV)         # the model's output layouts
+    vis = torch.empty(B, P, 1, 17, 3, device=DEV)
+    heat = torch.empty(B, P, 17, 56, 56, device=DEV)
+    plan.set_graphs(True)
+    try:
+        for it in range(4):                                 # eager, capture + launch, replay, replay
+            kpts.fill_(-1.0)
+            heat.fill_(-1.0)
+            plan.forward(img, boxes, kpts, vis, heat)
+            torch.cuda.synchronize()
+            assert torch.equal(kpts, ref["keypoints"]), it
+            assert torch.equal(heat, ref["heatmap"]), it
+            assert torch.equal(vis, ref["visibilities"]), it
+        # new data in the same buffers: the replay computes it
+        img2 = synthetic_images(B, 3, 256, 192, seed=83, device=DEV)
+        with torch.no_grad():
+            ref2 = m({"image": img2, "bboxes": boxes})      # eager (other output buffers)
+        img.copy_(img2)
+        plan.forward(img, boxes, kpts, vis, heat)
+        torch.cuda.synchronize()
+        assert torch.equal(kpts, ref2["keypoints"]) and torch.equal(heat, ref2["heatmap"])
+    finally:
+        plan.set_graphs(False)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "split", "mixed"])
 def test_c5_shape_dual_head_vs_oracle(precision):
     """BASELINE config C5's shape at a CPU-checkable batch: 384x288 input
