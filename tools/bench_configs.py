@@ -5,7 +5,8 @@ times C2, the metric's config).  One JSON line per config:
   C1  one 256x192 image with one box, as scripts/predict.py runs the forward:
       synchronous GPU latency (median of 50 after 10 warm-ups) beside the CPU
       reference path (the golden-pinned oracle, median of 5) on the host's
-      CPU share
+      CPU share; gpu_latency_graph_ms: the same forwards replayed as hipGraphs
+      (kpd_plan_set_graphs), with a check that their outputs are identical
 
   C3  B=256, 256x192, no boxes: person-detector glue (max 5 kept) + heatmap
       head + KEYPOINT_HEAD per ROI
@@ -67,7 +68,22 @@ def c1_latency(m, c, precision):
             torch.cuda.synchronize()
             if i >= 10:
                 ts.append(time.perf_counter() - t0)
+        # the same forwards replayed as hipGraphs (kpd_plan_set_graphs: opt-in,
+        # captured on the second call of a signature)
+        plan = m.native_plan(dev)
+        plan.set_graphs(True)
+        tg = []
+        for i in range(60):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            outg = m(batch)
+            torch.cuda.synchronize()
+            if i >= 10:
+                tg.append(time.perf_counter() - t0)
+        plan.set_graphs(False)
+        graph_same = all(torch.equal(out[k], outg[k]) for k in ("keypoints", "visibilities", "heatmap"))
     ts.sort()
+    tg.sort()
     ci = bench.host_cpu_info()
     torch.set_num_threads(ci["threads"])
     sd = {k: v.cpu() for k, v in m.state_dict().items()}
@@ -80,6 +96,7 @@ def c1_latency(m, c, precision):
     cs.sort()
     return {"config": "C1", "workload": c["desc"], "precision": precision,
             "gpu_latency_ms": round(ts[len(ts) // 2] * 1e3, 3), "gpu_latency_p90_ms": round(ts[int(len(ts) * .9)] * 1e3, 3),
+            "gpu_latency_graph_ms": round(tg[len(tg) // 2] * 1e3, 3), "graph_outputs_identical": graph_same,
             "cpu_reference_latency_ms": round(cs[2] * 1e3, 2), "cpu_threads": ci["threads"], "cpu_model": ci["model"],
             "max_abs_dkpt_vs_cpu": float((out["keypoints"].cpu() - ref["keypoints"]).abs().max())}
 
