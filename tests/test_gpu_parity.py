@@ -365,6 +365,21 @@ def test_graph_replay_matches_eager(model_sd, streams):
         plan.forward(img, boxes, kpts, vis, heat)
         torch.cuda.synchronize()
         assert torch.equal(kpts, ref2["keypoints"]) and torch.equal(heat, ref2["heatmap"])
+        # a larger batch re-carves the workspace: the captured graphs are
+        # stale (their kernels hold the old workspace addresses) and the
+        # original signature must run eagerly / be captured again
+        big = synthetic_images(2 * B, 3, 256, 192, seed=84, device=DEV)
+        with torch.no_grad():
+            out_big = m({"image": big, "bboxes": torch.cat([boxes, boxes])})
+            half = m({"image": big[B:], "bboxes": boxes})
+        assert torch.equal(out_big["keypoints"][B:], half["keypoints"])
+        for it in range(3):
+            kpts.fill_(-1.0)
+            heat.fill_(-1.0)
+            plan.forward(img, boxes, kpts, vis, heat)
+            torch.cuda.synchronize()
+            assert torch.equal(kpts, ref2["keypoints"]) and torch.equal(heat, ref2["heatmap"]), it
+            assert torch.equal(vis, ref2["visibilities"]), it
     finally:
         plan.set_graphs(False)
 
