@@ -80,6 +80,31 @@ def flops_per_image(H, W, P, in_ch=3):
             "hm_conv3": hm_convs[2] * P}
 
 
+def kh_flops_per_roi(c=128, fine=64, reg=32, vis=32, h=56, w=56):
+    """KEYPOINT_HEAD algorithmic flops per ROI (keypoint_head.py:9-90): 2*MAC
+    of its convs and linears at the ROI resolution (BN folded)."""
+    hw = h * w
+    f = 2.0 * hw * (c * (c // 2) + (c // 2))                        # spatial attention 1x1 C->C/2->1
+    f += 2.0 * hw * (c * fine * 9 + (c * fine if c != fine else 0))  # ResidualBlock(C->64) (+ downsample)
+    f += 2.0 * hw * (fine * reg * 9 + (fine * reg if fine != reg else 0))
+    f += 2.0 * hw * reg * (reg // 2) * 9                               # 3x3 32->16
+    f += 2.0 * ((reg // 2) * (h // 4) * (w // 4) * 256 + 256 * 34)    # regression linears
+    f += 2.0 * hw * c * vis * 9 + 2.0 * (vis * 16 * 128 + 128 * 51)   # visibility branch
+    return f
+
+
+def config_flops(H, W, P, detect):
+    """Per-image algorithmic flops of a C3 / C5 forward: backbone
+    + FPN level 0 + P x (heatmap head + KEYPOINT_HEAD) (+ the detector's 1x1
+    heads on the 56x56-pooled 128-channel level 0).  P may be fractional (the
+    mean detected persons per image)."""
+    fl = dict(flops_per_image(H, W, P))
+    kh = kh_flops_per_roi()
+    fl["keypoint_head"] = P * kh
+    fl["total"] += P * kh + (2.0 * 3136 * 128 * 45 if detect else 0.0)
+    return fl
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,9 +129,14 @@ def parse(argv=None):
                     help="N=1: also time the same workload at this many sub-batch streams (labelled "
                          "'alt_streams'; 0 = skip); the headline stays single-stream so the roofline's launch "
                          "times describe the kernel alone")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r03" / "pmc.json"),
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r04" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run (entries are "
                          "stamped with the hash of the kernel sources they were measured on)")
+    ap.add_argument("--c3", type=int, default=1,
+                    help="N=1: also run BASELINE C3 (B=256 256x192, person detector + NMS + heatmap head + "
+                         "KEYPOINT_HEAD) as the labelled 'configs.C3' object (0 = skip)")
+    ap.add_argument("--c3-only", action="store_true", help="run only the C3 object (profiling passes)")
+    ap.add_argument("--c3-cpu-sample", type=int, default=16, help="images in C3's CPU-baseline sample")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="test mode: no GPU; gloo ranks on the CPU run a stand-in forward through the same "
                          "launcher, barrier, timing and collation code (tests/test_bench_launch.py)")
@@ -151,25 +181,29 @@ def host_cpu_info():
     return info
 
 
-def cpu_baseline(sd, img, boxes, threads, warmups=3, runs=5, max_seconds=40.0):
+def cpu_baseline(sd, img, boxes, threads, warmups=3, runs=5, max_seconds=40.0, fwd=None):
     """The oracle (a plain-torch restatement of the reference forward with its
     per-box loop, golden-pinned) timed on this host: `warmups` untimed runs,
-    then the median of `runs` timed runs of the whole sample (fewer if one run
-    would push the total past max_seconds)."""
+    then the median of `runs` timed runs of the whole sample (more runs if
+    they fit in max_seconds, never fewer than 5).  `fwd` replaces the default
+    given-box forward (C3: dual head + detector glue)."""
     from oracle import kpd_oracle as O
     torch.set_num_threads(threads)
     batch = {"image": img, "bboxes": boxes}
+    if fwd is None:
+        def fwd():
+            return O.forward(sd, batch)
     t0 = time.perf_counter()
-    out = O.forward(sd, batch)        # first warmup: also the parity outputs
+    out = fwd()                       # first warmup: also the parity outputs
     once = time.perf_counter() - t0
     warmups = max(1, min(warmups, int(max_seconds / 3 / max(once, 1e-3))))
     for _ in range(warmups - 1):
-        O.forward(sd, batch)
+        fwd()
     runs = max(5, min(runs, int(max_seconds / max(once, 1e-3))))
     ts = []
     for _ in range(runs):
         t0 = time.perf_counter()
-        O.forward(sd, batch)
+        fwd()
         ts.append(time.perf_counter() - t0)
     ts.sort()
     med = ts[len(ts) // 2]
@@ -308,7 +342,7 @@ def stage_pass(m, plan, batch, iters):
     return st
 
 
-def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
+def roofline(precision, stages, fl, B, H, W, pmc, dom=None, tag=None):
     """Roofline of the dominant kernel (the longest single-kernel MFMA stage).
     achieved = ALGORITHMIC flops per launch (SURVEY §8(d)) / mean launch time;
     peak = dense MFMA peak of the dtype the kernel issues (f16/bf16 2.5 PF,
@@ -367,7 +401,8 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
         r["launches_note"] = note
     if exflop > 2.5 * flop:   # 3-product split: each fp32 MAC costs 3 MFMA products
         r["split_ceiling_frac"] = round(ach / (peak / 3.0), 4)
-    e = pmc.get(f"{dom}:{precision}") if pmc else None
+    # PMC entries: "<stage>:<precision>" for the headline C2, "<stage>:<precision>@<config>" otherwise
+    e = pmc.get(f"{dom}:{precision}" + (f"@{tag}" if tag else "")) if pmc else None
     if e:
         r["traffic"] = e.get("hbm_bytes_per_launch")
         r["traffic_unit"] = "HBM bytes/launch: rocprofv3 --pmc, 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)"
@@ -380,6 +415,118 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None):
         # the counters were measured on these kernel sources: false = stale (kernel changed since)
         r["pmc_current"] = e.get("src_hash") == cur
     return r
+
+
+C3 = dict(B=256, H=256, W=192, max_persons=5)
+
+
+def run_c3(a, dev, pmc, cpu=True):
+    """BASELINE config C3 on this GPU: B=256 synthetic 256x192 images without
+    boxes -> person detector (build-defined glue: pooled 1x1 heads, anchor
+    decode, threshold 0.3, NMS 0.3, max 5 kept) -> heatmap head + soft-argmax
+    and KEYPOINT_HEAD on every detected ROI.  Timed like the headline: W
+    warm-ups, K single-stream forwards with HIP events around the dominant
+    MFMA stage only; then the same at `--alt-streams` sub-batch streams
+    (throughput only).  CPU baseline: the oracle's full C3 forward (its own FPN
+    level 0 -> its detector -> dual head) on the first `--c3-cpu-sample`
+    images, 3 warm-ups + median of 5."""
+    from dll import _native
+    from dll.configs import KeypointHeadConfig, ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_images, synthetic_state_dict
+    B, H, W = C3["B"], C3["H"], C3["W"]
+    m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
+                                 TrainingConfig(), precision=a.precision, dual_head=True,
+                                 max_persons=C3["max_persons"], streams=1)
+    sd = synthetic_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(dev).eval()
+    img_cpu = synthetic_images(B, 3, H, W, seed=4321)
+    img = img_cpu.to(dev)
+    plan = m.native_plan(dev)
+
+    def step():
+        return m(img)           # plain tensor: the detector branch
+
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            step()
+    bd = stage_pass(m, plan, img, 1)
+    launches = {k: v[1] for k, v in bd.items()}
+    mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
+    dom = max((k for k in bd if k in mfma_stages), key=lambda k: bd[k][0])
+    plan.timing(True, stage=dom)
+    el, out = run_steps(a.steps, 0, step, False)
+    plan.timing(False)
+    dms, dn = plan.timing_query(dom)
+    stages = {k: v[0] for k, v in bd.items()}
+    nl = max(1, launches[dom])           # launches of a stage per forward (one per pass)
+    if dn:
+        stages[dom] = dms / dn
+    rois = int((out["box_scores"] > 0).sum())
+    P_eff = rois / B                     # detected persons per image (the heads run on these ROIs)
+    fl = config_flops(H, W, P_eff, True)
+    roof = roofline(a.precision, stages, fl, B / nl, H, W, pmc, dom, tag="C3")
+    roof["launches_timed"] = dn
+    roof["images_per_launch"] = B / nl
+    roof["rois_per_launch"] = rois / nl
+    roof["timing"] = "HIP events around every launch of this stage inside the timed region (single stream)"
+    res = {"workload": f"C3: batch {B}, {H}x{W}x3, no boxes: person detector (pooled 1x1 heads, anchor decode, "
+                       f"conf 0.3, NMS 0.3, max {C3['max_persons']}) + heatmap head + soft-argmax + KEYPOINT_HEAD "
+                       "per detected ROI",
+           "value": round(B * a.steps / el, 2), "unit": "images/s", "ms_per_step": round(el / a.steps * 1e3, 4),
+           "steps": a.steps, "warmup": a.warmup, "streams_per_gpu": 1, "precision": a.precision,
+           "rois": rois, "persons_per_image": round(P_eff, 3),
+           "gflop_per_image": round(fl["total"] / 1e9, 3),
+           "achieved_tflops_total": round(fl["total"] * B * a.steps / el / 1e12, 2),
+           "roofline": roof, "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+           "stage_launches_per_forward": launches}
+    if "keypoint_head" in stages:
+        res["keypoint_head_tflops"] = round(fl["keypoint_head"] * B / nl / (stages["keypoint_head"] * 1e-3) / 1e12, 2)
+    if a.alt_streams and a.alt_streams != 1:
+        m.streams = a.alt_streams
+        el2, out2 = run_steps(a.steps, a.warmup, step, False)
+        m.streams = 1
+        res["alt_streams"] = {"streams_per_gpu": a.alt_streams, "value": round(B * a.steps / el2, 2),
+                              "ms_per_step": round(el2 / a.steps * 1e3, 4),
+                              "outputs_identical": all(torch.equal(out[k], out2[k]) for k in
+                                                       ("keypoints", "visibilities", "kh_keypoints",
+                                                        "box_scores"))}
+    if cpu and a.c3_cpu_sample > 0:
+        from oracle import kpd_oracle as O
+        ci = host_cpu_info()
+        S = min(a.c3_cpu_sample, B)
+        sdc = {k: v.cpu() for k, v in m.state_dict().items()}
+        xs = img_cpu[:S]
+
+        def fwd():
+            return O.forward(sdc, {"image": xs}, dual_head=True,
+                             detect=dict(conf_threshold=0.3, iou_threshold=0.3, max_persons=C3["max_persons"]))
+        ref, rate, proto = cpu_baseline(sdc, xs, None, ci["threads"], fwd=fwd)
+        res["cpu_baseline"] = {
+            "value": round(rate, 3), "unit": "images/s", "cores": ci["threads"], "kind": "port",
+            "sample": f"{S} images of the same C3 workload, oracle/kpd_oracle.py (its own FPN level 0 -> detector "
+                      f"glue -> heatmap head + KEYPOINT_HEAD), {proto['warmups']} warmups + median of "
+                      f"{proto['runs']} runs",
+            "protocol": proto, "cpu_model": ci["model"]}
+        res["gpu_vs_cpu"] = round(res["value"] / rate, 1)
+        gb = torch.stack([out["boxes"][i].cpu() for i in range(S)])
+        gk = out["keypoints"][:S].cpu()
+        d = (gk - ref["keypoints"]).norm(dim=-1)
+        res["parity"] = {
+            "images": S, "pck@0.5": float((d <= 0.5).float().mean()), "pck@0.002": float((d <= 0.002).float().mean()),
+            "max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
+            "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
+            "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
+            "max_abs_dkh_kpt": float((out["kh_keypoints"][:S].cpu() - ref["kh_keypoints"]).abs().max()),
+            "max_abs_dkh_vis": float((out["kh_visibilities"][:S].cpu() - ref["kh_visibilities"]).abs().max()),
+            "kept_persons_equal": bool(torch.equal((out["box_scores"][:S].cpu() > 0).sum(1),
+                                                   (ref["box_scores"] > 0).sum(1))),
+            "max_abs_dbox": float((gb - torch.stack(list(ref["boxes"]))).abs().max()),
+            "max_abs_dscore": float((out["box_scores"][:S].cpu() - ref["box_scores"]).abs().max())}
+    del m, plan, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def kernel_src_hash():
@@ -421,6 +568,18 @@ def main(argv=None):
     from dll.configs import ModelConfig, TrainingConfig
     from dll.models import MultiPersonKeypointModel
     from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+
+    pmc = None
+    pj = Path(a.pmc_json)
+    if pj.exists():
+        try:
+            pmc = json.loads(pj.read_text())
+        except ValueError:
+            pmc = None
+    if a.c3_only:
+        if rank == 0:
+            print(json.dumps({"configs": {"C3": run_c3(a, dev, pmc, cpu=not a.no_cpu_baseline)}}), flush=True)
+        return
 
     def build(precision):
         m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=precision, streams=a.streams)
@@ -468,13 +627,6 @@ def main(argv=None):
     el = max(per_rank)
 
     fl = flops_per_image(a.height, a.width, P)
-    pmc = None
-    pj = Path(a.pmc_json)
-    if pj.exists():
-        try:
-            pmc = json.loads(pj.read_text())
-        except ValueError:
-            pmc = None
     roof = roofline(a.precision, stages, fl, Bl, a.height, a.width, pmc, dom)
     if roof:
         roof["forwards_before_timed"] = a.warmup + 1     # --warmup + the one stage-breakdown forward
@@ -562,6 +714,11 @@ def main(argv=None):
                           "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
                           "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
                           "images": S}
+    if world == 1 and a.c3:
+        # BASELINE C3 (the north_star's full pipeline) as a labelled object beside the C2 headline
+        del m, plan
+        torch.cuda.empty_cache()
+        line["configs"] = {"C3": run_c3(a, dev, pmc, cpu=not a.no_cpu_baseline)}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

@@ -193,15 +193,29 @@ int kpd_plan_set_streams(kpd_plan* plan, int n);
  * Default: off (KPD_GRAPH=1 in the environment: on).  Measured at 64 and 1
  * images back to back, replay is no faster than the eager launches (the GPU
  * is the bound there); one synchronous 1-image forward (C1) took 0.62 ms
- * replayed against 0.67 ms eager. */
+ * replayed against 0.67 ms eager.
+ * The signature includes every buffer address: replay needs caller-owned
+ * buffers reused from call to call (a caller that allocates new outputs per
+ * call gets a new signature, i.e. an eager run, whenever an address changes).
+ * enable = 2: on, and the next capture is abandoned as if it had failed (the
+ * call then runs eagerly with the plan's workspace state restored) -- a test
+ * hook for that recovery path. */
 int kpd_plan_set_graphs(kpd_plan* plan, int enable);
 
 /* Diagnostics (not part of the reference interface): times the LDS-DMA 3x3
  * conv (conv_glds.hip) on synthetic operands, N x H x W pixels, cin -> cout;
  * split != 0 selects the fp32-accurate FPN level-0 form (cin = cout = 128).
  * dbg: 0 full kernel, 1 without the K-loop loads, 2 without the MFMAs,
- * 4 with an L2-resident A working set.  *ms = mean time per launch. */
+ * 4 with an L2-resident A working set.  *ms = mean time per launch.  The
+ * ablations (dbg != 0) exist only in a diagnostic build (kpd_build_flags). */
 int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cout, int dbg, int iters, float* ms);
+
+/* Build flags of this library: bit 0 (KPD_BUILD_DIAG) = diagnostic build
+ * (make DIAG=1), which reads the KPD_* A/B and ablation switches and the
+ * KPD_STAMPS phase stamps from the environment.  The default build reads
+ * none of them (only KPD_GRAPH, the kpd_plan_set_graphs default). */
+#define KPD_BUILD_DIAG 1
+int kpd_build_flags(void);
 
 /* ---- Stand-alone operators: the reference's submodule forwards and helper
  * functions, for callers that use them outside MultiPersonKeypointModel.forward.

@@ -1401,8 +1401,8 @@ hipError_t launch_lateral_stream(const float* in, int cin_p, const float* w, con
   if (cin_p != 16 && cin_p != 32) return hipErrorInvalidValue;
   const int M = N * H * W;
   const int chunks = (M + 16 * kLatPix - 1) / (16 * kLatPix);
-  static const int blocks_env = getenv("KPD_LAT_BLOCKS") ? atoi(getenv("KPD_LAT_BLOCKS")) : kLatBlocks;
-  static const int nt_env = getenv("KPD_LAT_NT") ? atoi(getenv("KPD_LAT_NT")) : 0;
+  static const int blocks_env = kpd_diag_env("KPD_LAT_BLOCKS") ? atoi(kpd_diag_env("KPD_LAT_BLOCKS")) : kLatBlocks;
+  static const int nt_env = kpd_diag_env("KPD_LAT_NT") ? atoi(kpd_diag_env("KPD_LAT_NT")) : 0;
   const int nblk = std::max(1, std::min(chunks, blocks_env));
 #define LAT(C4) hipLaunchKernelGGL(lateral_stream_kernel<C4>, dim3(nblk), dim3(256), 0, st, in, w, bias, res, H, \
                                   W, rh, rw, M, static_cast<float*>(out), nt_env)
@@ -1431,7 +1431,7 @@ int fir_pick_rows(FirArgs& a, int K, int S) {
   if (a.cin_p % 4 || a.Ep % FIR_CS || a.cout_p % 8 || (a.res && (S != 1 || a.cin_p != a.cout_p)) ||
       a.cin_p * FIR_CS > 1024 || FIR_CS * a.cout_p > 1024 || K * K * FIR_CS / 4 > 256)
     return 0;
-  static const int th_env = getenv("KPD_FIR_TH") ? atoi(getenv("KPD_FIR_TH")) : 0;   // A/B sweeps
+  static const int th_env = kpd_diag_env("KPD_FIR_TH") ? atoi(kpd_diag_env("KPD_FIR_TH")) : 0;   // A/B sweeps
   for (int th = std::min(a.Ho, th_env > 0 ? th_env : 16); th >= 1; --th) {
     a.TH = th;
     const int units = (th * a.Wo + 1) / 2 * (a.cout_p / 8);
@@ -1518,7 +1518,7 @@ hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
     return hipErrorInvalidValue;
   // the 192-pixel maps split their rows over two workgroups (384 instead of
   // 192 workgroups at 64 images; each recomputes the cheap excitation)
-  static const int msplit_env = getenv("KPD_SEPROJ_MSPLIT") ? atoi(getenv("KPD_SEPROJ_MSPLIT")) : 2;
+  static const int msplit_env = kpd_diag_env("KPD_SEPROJ_MSPLIT") ? atoi(kpd_diag_env("KPD_SEPROJ_MSPLIT")) : 2;
   const int msplit = mt_all == 12 ? std::max(1, msplit_env) : 1;
   const int mt = (mt_all + msplit - 1) / msplit;
   SeProjArgs b = a;
@@ -1527,7 +1527,7 @@ hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
   // 12.1 -> 9.6 us per launch.  The 192-pixel maps (6 row tiles per
   // workgroup) measured 13.5 -> 16.9 us with eight, so they keep four.
   // KPD_SEPROJ_NWV = 4 / 8 forces one (A/B).
-  static const int nwv_env = getenv("KPD_SEPROJ_NWV") ? atoi(getenv("KPD_SEPROJ_NWV")) : 0;
+  static const int nwv_env = kpd_diag_env("KPD_SEPROJ_NWV") ? atoi(kpd_diag_env("KPD_SEPROJ_NWV")) : 0;
   const int nwv = nwv_env == 4 || nwv_env == 8 ? nwv_env : (mt == 3 ? 8 : 4);
   const size_t lds_m = 4 * ((size_t)a.Ep + 256 + std::max({(size_t)nwv * mt * 16 * a.NT, (size_t)a.nsl * a.sq,
                                                              std::max<size_t>(1, std::min<size_t>(16, 256 / (a.C / 4))) * a.C}));
@@ -1572,7 +1572,7 @@ hipError_t launch_se16_proj(const float* d, int N, int npx, int ntiles, const fl
 }
 
 bool pw_small_ok(const ConvArgs& a) {
-  static const bool off = getenv("KPD_NO_PWSMALL") != nullptr;   // A/B switch
+  static const bool off = kpd_diag_env("KPD_NO_PWSMALL") != nullptr;   // A/B switch
   // large outputs keep the generic kernel's LDS-staged 16-byte stores: lateral
   // 1 (6.3 M outputs at 64 images) measured 18.9 us here vs 17.6 us there;
   // lateral 2 (1.6 M) 8.2 vs 17, the last conv (1.8 M) 12.9 vs 18

@@ -1766,7 +1766,7 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
           hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         ncu = 256;
     }
-    static const int bm_env = getenv("KPD_HMCONV_BM") ? atoi(getenv("KPD_HMCONV_BM")) : 0;   // A/B
+    static const int bm_env = kpd_diag_env("KPD_HMCONV_BM") ? atoi(kpd_diag_env("KPD_HMCONV_BM")) : 0;   // A/B
     auto cost = [&](long bm) { return ((rows + bm - 1) / bm * (a.cout / bn) + ncu - 1) / ncu * bm; };
     // conv 1 / 2 (cin 64 / 256) always take 224-row tiles: those are the
     // instances with the input channels as a compile-time constant (the
@@ -1777,10 +1777,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
                    : bm_env == 224 || bm_env == BM ? bm_env
                    : (spec || cost(224) < cost(BM)) ? 224 : BM;
     const dim3 grid((unsigned)(((rows + bm - 1) / bm) * (a.cout / bn)));
-    static const int dbg = getenv("KPD_HMCONV_DBG") ? atoi(getenv("KPD_HMCONV_DBG")) : 0;   // ablations only
-    static const int hm_tps = getenv("KPD_HM3_TPS1") ? -1 : 0;   // A/B: conv 3 with one tap per K-step
-    static const bool hm_db = getenv("KPD_HM3_NODB") == nullptr;  // A/B: conv 3 single fragment set
-    static const bool hm_stagger = getenv("KPD_HM_NOSTAGGER") == nullptr;   // A/B: staggered DMA issue (split)
+    static const int dbg = kpd_diag_env("KPD_HMCONV_DBG") ? atoi(kpd_diag_env("KPD_HMCONV_DBG")) : 0;   // ablations only
+    static const int hm_tps = kpd_diag_env("KPD_HM3_TPS1") ? -1 : 0;   // A/B: conv 3 with one tap per K-step
+    static const bool hm_db = kpd_diag_env("KPD_HM3_NODB") == nullptr;  // A/B: conv 3 single fragment set
+    static const bool hm_stagger = kpd_diag_env("KPD_HM_NOSTAGGER") == nullptr;   // A/B: staggered DMA issue (split)
     a.stagger = hm_stagger ? 1 : 0;
 #define HMK(...) hipLaunchKernelGGL((hmconv_kernel<__VA_ARGS__>), grid, dim3(NT), 0, st, a)
     // conv 3 (BN 64, one tile per CU round): the rounds after the last full
@@ -1789,10 +1789,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // tiles and the rest goes out as 128-row tiles in one extra launch
     // (146 at 64 ROIs: a half-length round).  Tile sizes never change the
     // arithmetic of a row (same K order), so results are unchanged.
-    static const bool no_tail = getenv("KPD_HM3_NOTAIL") != nullptr;   // A/B
+    static const bool no_tail = kpd_diag_env("KPD_HM3_NOTAIL") != nullptr;   // A/B
     // A/B (KPD_HM3_NW4=1): conv 3 split as 4 waves of 64 x 64 -- 1.5x fewer LDS
     // bytes per MFMA, but one wave per SIMD hides no latency: 0.204 vs 0.173 ms
-    static const bool hm3_nw4 = getenv("KPD_HM3_NW4") != nullptr;
+    static const bool hm3_nw4 = kpd_diag_env("KPD_HM3_NW4") != nullptr;
     a.m_off = 0;
     if (fin && !dbg && !no_tail && !a.stamps && (!split || (a.cin == 256 && hm_db))) {
       const long nfull = rows / BM, F = nfull / ncu * ncu, rem = rows - F * BM, H = (rem + 127) / 128;
@@ -1821,7 +1821,7 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // 0.86 as long): 0.528 -> 0.515 ms.  Conv 1 (18 K-steps a tile, so the
     // per-tile prologue / epilogue dominate) measured 2 % slower with it.
     // Same K order per row: results unchanged.
-    static const bool no_tail12 = getenv("KPD_HM12_NOTAIL") != nullptr;   // A/B
+    static const bool no_tail12 = kpd_diag_env("KPD_HM12_NOTAIL") != nullptr;   // A/B
     if (split && !fin && bn == 256 && bm == 224 && a.cin == 256 && !dbg && !no_tail12 && !a.stamps) {
       const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
       if (F > 0 && rem > 0 && H <= ncu) {
@@ -1835,12 +1835,15 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
         continue;
       }
     }
+#if KPD_DIAG
     if (split && dbg) {   // ablations (KPD_HMCONV_DBG=1: no MFMA, 2: no K-loop DMA); wrong results by design
       if (fin && dbg == 1) HMK(64, 2, 1, BM, true, 256, 3, true);   // the production conv 3 variant
       else if (fin) HMK(64, 2, 2, BM, true, 256, 3, true);
       else if (dbg == 1) HMK(256, 2, 1, 224, true, 256);
       else HMK(256, 2, 2, 224, true, 256);
-    } else if (split) {
+    } else
+#endif
+    if (split) {
       if (fin && a.cin == 256 && hm_db && hm3_nw4)
         hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 256, 3, true, 4>), grid, dim3(256), 0, st, a);
       else if (fin && a.cin == 256 && hm_db) HMK(64, 2, 0, BM, true, 256, 3, true);
@@ -1856,8 +1859,10 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     else if (bn == 256 && bm == 224 && dbg == 0 && a.cin == 64) HMK(256, 2, 0, 224, false, 64);
     else if (bn == 256 && bm == 224 && dbg == 0 && a.cin == 256) HMK(256, 2, 0, 224, false, 256);
     else if (bn == 256 && bm == 224 && dbg == 0) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224>), grid, dim3(NT), 0, st, a);
+#if KPD_DIAG
     else if (bn == 256 && dbg == 1) hipLaunchKernelGGL((hmconv_kernel<256, 2, 1>), grid, dim3(NT), 0, st, a);
     else if (bn == 256 && dbg == 2) hipLaunchKernelGGL((hmconv_kernel<256, 2, 2>), grid, dim3(NT), 0, st, a);
+#endif
     else if (bn == 256) hipLaunchKernelGGL((hmconv_kernel<256, 2>), grid, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((hmconv_kernel<128, 4>), grid, dim3(NT), 0, st, a);
 #undef HMK
@@ -1884,20 +1889,25 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  static const int grid_env = getenv("KPD_FPN0X_GRID") ? atoi(getenv("KPD_FPN0X_GRID")) : 0;   // A/B
+  static const int grid_env = kpd_diag_env("KPD_FPN0X_GRID") ? atoi(kpd_diag_env("KPD_FPN0X_GRID")) : 0;   // A/B
   const long grid = std::min<long>(tiles, grid_env > 0 ? grid_env : ncu);
-  static const int dbg = getenv("KPD_FPN0X_DBG") ? atoi(getenv("KPD_FPN0X_DBG")) : 0;   // ablations only
-  static const bool stagger = getenv("KPD_FPN0X_NOSTAGGER") == nullptr;                   // A/B
+#if KPD_DIAG
+  static const int dbg = kpd_diag_env("KPD_FPN0X_DBG") ? atoi(kpd_diag_env("KPD_FPN0X_DBG")) : 0;   // ablations only
+#endif
+  static const bool stagger = kpd_diag_env("KPD_FPN0X_NOSTAGGER") == nullptr;                   // A/B
   Fpn0xArgs b = a;
   b.stagger = stagger ? 1 : 0;
   // non-temporal output (KPD_FPN0X_NT=0: off): FETCH_SIZE 216 -> 162 MB per launch (the stores no longer
   // evict the weights and input rows from L2), -1 % time
-  static const int out_nt = getenv("KPD_FPN0X_NT") ? atoi(getenv("KPD_FPN0X_NT")) : 1;
+  static const int out_nt = kpd_diag_env("KPD_FPN0X_NT") ? atoi(kpd_diag_env("KPD_FPN0X_NT")) : 1;
   b.out_nt = out_nt;
+#if KPD_DIAG   // ablations (KPD_FPN0X_DBG=1: no MFMA, 2: no K-loop DMA, 4: one output piece); wrong results by design
   if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, b);
-  else hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, b);
+  else
+#endif
+  hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   return hipGetLastError();
 }
 
@@ -1953,6 +1963,7 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
     hipError_t e = hipSuccess;
     switch (dbg) {
       case 0: e = bench_launch<0>(a, split, 0); break;
+#if KPD_DIAG   // ablation variants (wrong results by design): diagnostic builds only
       case 1: e = bench_launch<1>(a, split, 0); break;
       case 2: e = bench_launch<2>(a, split, 0); break;
       case 4: e = bench_launch<4>(a, split, 0); break;
@@ -1962,6 +1973,7 @@ extern "C" int kpd_bench_conv16(int split, int N, int H, int W, int cin, int cou
       case 24: e = bench_launch<24>(a, split, 0); break;
       case 128: e = bench_launch<128>(a, split, 0); break;
       case 4096: e = bench_launch<4096>(a, split, 0); break;
+#endif
       default: e = hipErrorInvalidValue;
     }
     if (e != hipSuccess) goto done;

@@ -772,15 +772,15 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
                             int R, int P, float* roi, float* roi_stats, hipStream_t st, unsigned long long* stamps) {
   // the stage holds at most the map's width of interpolated columns: sized to
   // that (64 channels at Wf 96: 24 KB, 6 workgroups per CU instead of 3)
-  static const bool full_cap = getenv("KPD_ROI_FULLCAP") != nullptr;   // A/B: the fixed 50 KB stage
+  static const bool full_cap = kpd_diag_env("KPD_ROI_FULLCAP") != nullptr;   // A/B: the fixed 50 KB stage
   if (topk) {
-    static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
+    static const bool direct = kpd_diag_env("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
     const int cap = direct ? 0 : full_cap ? kRoiStageFloats : std::min(kRoiStageFloats, Wf * TOPK);
     hipLaunchKernelGGL((roi_align_kernel<1>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, topk, boxes, P,
                        roi, roi_stats, cap, stamps);
   } else {
     if (Cf != 2 * TOPK) return hipErrorInvalidValue;
-    static const bool direct = getenv("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
+    static const bool direct = kpd_diag_env("KPD_ROI_DIRECT") != nullptr;   // A/B: no LDS stage
     const int cap = direct ? 0 : full_cap ? kRoiStageFloats : std::min(kRoiStageFloats, Wf * 2 * TOPK);
     hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
                        roi, nullptr, cap, stamps);

@@ -3,6 +3,24 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+// Diagnostic switches -- A/B variants of measured changes, ablations that are
+// wrong by design (KPD_*_DBG), phase stamps (KPD_STAMPS) -- are read from the
+// environment only in a diagnostic build (make DIAG=1, -DKPD_DIAG=1).  The
+// default libkpd.so never reads them: kpd_diag_env() is a constant null, the
+// switches fold away and a stray variable on a serving box changes nothing.
+#ifndef KPD_DIAG
+#define KPD_DIAG 0
+#endif
+static inline const char* kpd_diag_env(const char* name) {
+#if KPD_DIAG
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

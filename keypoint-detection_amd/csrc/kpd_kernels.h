@@ -182,37 +182,6 @@ struct ExDwArgs {
 };
 size_t exdw_lds_bytes(const ExDwArgs& a, int K);
 hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st);
-// Coarse MobileNet body in one launch (cbody.hip, cbody_kernel): features.5..11
-// (squeeze-excitation inverted residuals) and features.12 (1x1 96 -> 576 +
-// hardswish), one 512-thread workgroup per image, activations in LDS, the
-// 1x1 convs as f16 hi/lo x3 MFMA products (fp32-accurate), depthwise and SE
-// in fp32.
-constexpr int kCbMaxLayers = 7;
-struct CbLayer {
-  int Hi, Wi, Ho, Wo, k, s;
-  int cin_p, kc_in;            // input channels (X row stride, multiple of 16), 32-channel K chunks
-  int Ep, EpK, C;              // expanded channels padded to 16 / 32, true expanded channels (SE)
-  int cout_p, act, res, se, sq;
-  const _Float16* we; int we_exp; const float* be;   // expand [Ep][kc_in][hi32 | lo32] (* 2^we_exp), bias [Ep]
-  const float *wd, *bd;        // depthwise [k*k][Ep], [Ep]
-  const float *w1, *b1, *w2t, *b2;   // SE fc1 [sq][C], fc2 transposed [sq][C]
-  const _Float16* wp; int wp_exp; const float* bp;   // project [cout_p][EpK/32][hi32 | lo32], bias [cout_p]
-  float* tap;                  // optional: the block output also to [N][Ho*Wo][cout_p] (FPN tap)
-};
-struct CbodyArgs {
-  const float* x;              // features.4 output [N][Hi*Wi][cin_p of layer 0]
-  int nl;
-  CbLayer L[kCbMaxLayers];
-  const _Float16* wl; int wl_exp; const float* bl;   // features.12 [576][kc][hi32 | lo32], bias
-  int last_cin_p, last_kc, last_cout;
-  float* tap3;                 // [N][P][576]
-  float* dscr;                 // per-image depthwise-output scratch
-  long dscr_floats;            // floats per image
-  unsigned long long* stamps;  // diagnostic phase stamps [N][128] (KPD_STAMPS), normally null
-  int dbg;                     // ablations (KPD_CBODY_DBG): 1 = no depthwise-output stores (wrong results)
-};
-size_t cbody_lds_bytes(const CbodyArgs& a);
-hipError_t launch_cbody(const CbodyArgs& a, int N, hipStream_t st);
 // SE excitation (from exdw_kernel's fc1 partials) + project 1x1 + residual
 // (body_kernels.hip, seproj_kernel)
 struct SeProjArgs {

@@ -90,7 +90,7 @@ struct DevConv {
   void* ws = nullptr;
   int w_exp = 0;
   float bc = 0.f, bs = 0.f;
-  int ws_kc = 0;   // 1x1 split copy (cbody_kernel): f16 [cout_p][ws_kc][hi32 | lo32], K zero-padded to 32
+  int ws_kc = 0;   // 1x1 split copy (kh_att2_kernel): f16 [cout_p][ws_kc][hi32 | lo32], K zero-padded to 32
 };
 struct DevDW { int C = 0, Cp = 0, k = 3, s = 1, act = 0; float* w = nullptr; float* b = nullptr; };
 struct DevSE { int C = 0, Cp = 0, sq = 0; float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr; };
@@ -137,8 +137,6 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   float* heat = nullptr;  // internal heat buffer when the caller passes NULL
   float* splitk = nullptr;  // split-K partial sums for small-M 1x1 convs (kSplitKFloats)
   float* pool = nullptr;    // [B][1024] SE channel means from the fused expand+depthwise kernel
-  float* cbd = nullptr;     // [B][cbd_floats] depthwise-output scratch of cbody_kernel (coarse body)
-  long cbd_floats = 0;
   float* separt = nullptr;  // [B][kSePartFloats] SE fc1 partials (exdw_kernel -> seproj_kernel)
   float* sc = nullptr;    // split FPN scale inputs: per-image max|tap0| [B], max|lateral1| [B] (amax_publish_img)
   bool sc_dirty = true;   // sc may hold a previous forward's maxima (topk_kernel re-zeroes it)
@@ -239,12 +237,13 @@ struct kpd_plan {
   // hipGraph replay of whole forwards (KPD_GRAPH=1): one executable graph per
   // call signature (shapes, flags, every buffer address, stream), valid while
   // the workspace carve and the weights are the ones it was captured on
-  struct GraphEntry { hipGraphExec_t exec = nullptr; long epoch = -1; int seen = 0; };
+  // never: instantiation failed for this signature -> always eager
+  struct GraphEntry { hipGraphExec_t exec = nullptr; long epoch = -1; int seen = 0; bool never = false; };
   std::map<std::vector<uintptr_t>, GraphEntry> graphs;
   long ws_epoch = 0;             // bumped whenever a workspace is re-carved or the weights re-packed
   bool use_graphs = getenv("KPD_GRAPH") != nullptr && atoi(getenv("KPD_GRAPH")) != 0;   // kpd_plan_set_graphs (KPD_GRAPH=1: on)
   hipStream_t graph_st = nullptr;   // capture stream (the caller's may be the legacy default stream)
-  hipEvent_t graph_ev = nullptr;
+  bool graph_abandon_next = false;  // kpd_plan_set_graphs(p, 2): abandon the next capture (tests the retry)
   hipStream_t sub_st_pri[kMaxSub] = {};   // high-priority sub-batch streams (KPD_PIPE_PRI)
   std::map<std::string, std::pair<const void*, size_t>> debug;
   unsigned long long* stamps = nullptr;   // KPD_STAMPS diagnostic buffer (kStampWords)
@@ -440,7 +439,8 @@ int pack_split_hm(kpd_plan* p, DevConv& dc) {
   return KPD_OK;
 }
 
-// Split (fp32-accurate) copy of a 1x1 conv for cbody_kernel: the packed fp32
+// Split (fp32-accurate) copy of a 1x1 conv (kh_att2_kernel: KEYPOINT_HEAD's
+// spatial-attention 1x1 128 -> 64): the packed fp32
 // weights [cout_p][cin_p] scaled by 2^w_exp (max|w| < 2^15), each value as f16
 // hi + lo, stored per 32 input channels as [hi32 | lo32] (K zero-padded to 32).
 int pack_split_1x1(kpd_plan* p, DevConv& dc) {
@@ -638,7 +638,6 @@ int pack_fpn0x(kpd_plan* p, const DevConv& dc, const DevConv& lat0) {
 constexpr long kSplitKFloats = 1L << 22;   // 16 MiB of split-K partials per workspace
 constexpr int kFuseMaxPix = 32 * 24;        // input maps up to this size take the fused expand+depthwise
 constexpr int kSePartFloats = 8192;         // per image: (Ep / CS) slices x sq fc1 partials
-constexpr int kCbFirst = 4;                 // cbody_kernel runs features.(kCbFirst + 1) .. 12
 
 struct Carver {
   char* base;
@@ -655,7 +654,7 @@ struct Carver {
 // mixed precision runs the HeatmapHead convs on zero-bordered ROI maps
 // (hmconv_kernel); KPD_NO_HMCONV=1 keeps the unpadded generic conv (A/B)
 bool hm_padded(const kpd_plan* p) {
-  static const bool off = getenv("KPD_NO_HMCONV") != nullptr;
+  static const bool off = kpd_diag_env("KPD_NO_HMCONV") != nullptr;
   return (p->precision == KPD_PRECISION_MIXED || p->precision == KPD_PRECISION_SPLIT) && !off;
 }
 
@@ -680,11 +679,6 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
   w.sc = c.take<float>((size_t)2 * B * kAmaxStride);
   w.splitk = c.take<float>(kSplitKFloats);
   w.pool = c.take<float>((size_t)B * 1024);
-  w.cbd_floats = 0;
-  if (p->precision != KPD_PRECISION_FP32)
-    for (int i = kCbFirst; i < 11; ++i)
-      w.cbd_floats = std::max(w.cbd_floats, (long)d.h[i + 1] * d.w[i + 1] * ((pad16(p->bn[i].cfg.exp) + 31) / 32 * 32));
-  w.cbd = c.take<float>((size_t)B * w.cbd_floats);
   w.separt = c.take<float>((size_t)B * kSePartFloats);
   w.topk = c.take<int32_t>((size_t)B * 64);
   w.scores = c.take<float>((size_t)B * 128);
@@ -862,6 +856,7 @@ extern "C" {
 
 const char* kpd_last_error(void) { return g_err.c_str(); }
 const char* kpd_version(void) { return "kpd 0.1 gfx950"; }
+int kpd_build_flags(void) { return KPD_DIAG ? KPD_BUILD_DIAG : 0; }
 
 int kpd_plan_create(int device, int in_channels, kpd_plan** out) {
   if (!out) return fail(KPD_EINVAL, "out is NULL");
@@ -905,7 +900,6 @@ void kpd_plan_destroy(kpd_plan* p) {
   for (auto& kv : p->graphs)
     if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
   if (p->graph_st) (void)hipStreamDestroy(p->graph_st);
-  if (p->graph_ev) (void)hipEventDestroy(p->graph_ev);
   for (auto& kv : p->timers)
     for (auto& e : kv.second.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   (void)hipSetDevice(cur);
@@ -999,13 +993,6 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     chk(pack_conv(p, pj + ".0.weight", "", pj + ".1", 1e-3, 1, false, bn.project, missing));
   }
   chk(pack_conv(p, F + "12.0.weight", "", F + "12.1", 1e-3, 1, false, p->last, missing));
-  if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty()) {   // cbody_kernel operands
-    for (int i = kCbFirst; i < 11; ++i) {
-      if (p->bn[i].has_exp) chk(pack_split_1x1(p, p->bn[i].expand));
-      chk(pack_split_1x1(p, p->bn[i].project));
-    }
-    chk(pack_split_1x1(p, p->last));
-  }
   }
   if (p->has_fpn) {
   for (int i = 0; i < 4; ++i) {
@@ -1135,7 +1122,7 @@ int kpd_plan_finalize(kpd_plan* p, int precision) {
     // 128 -> 64 -> 32 with downsamples, 3x3 32 -> 16, visibility 128 -> 32)
     const bool std_kh = p->kh_rb1.cin == 128 && p->kh_rb1.cout == 64 && p->kh_ds1.w && p->kh_rb2.cin == 64 &&
                         p->kh_rb2.cout == 32 && p->kh_ds2.w && p->kh_c3.cin == 32 && p->kh_v1.cin == 128;
-    static const bool no_kh_split = getenv("KPD_NO_KH_SPLIT") != nullptr;   // A/B switch
+    static const bool no_kh_split = kpd_diag_env("KPD_NO_KH_SPLIT") != nullptr;   // A/B switch
     if (precision != KPD_PRECISION_FP32 && rc == KPD_OK && missing.empty() && std_kh && !no_kh_split) {
       chk(pack_split_kh(p, p->kh_s[0], 128, 128, 10, {{&p->kh_rb1, &p->kh_ds1, p->kh_bn1a_s, p->kh_bn1a_t, 0},
                                                       {&p->kh_v1, nullptr, nullptr, nullptr, 64}}));
@@ -1173,7 +1160,7 @@ static int max_pass_images(int H, int W) {
 // FPN level 0 by linearity applies (mixed precision, packed composite weights,
 // lateral 1 an exact 4x nearest upsample of the level-0 grid)
 static bool fpn0x_ok(const kpd_plan* p, const Dims& d) {
-  static const bool no_lin = getenv("KPD_NO_FPN0X") != nullptr;   // A/B switch
+  static const bool no_lin = kpd_diag_env("KPD_NO_FPN0X") != nullptr;   // A/B switch
   return p->precision != KPD_PRECISION_FP32 && !no_lin && p->fpn0x.w0 != nullptr && d.Hf == 4 * d.h[3] &&
          d.Wf == 4 * d.w[3] && (long)((d.h[3] * d.w[3] + 255) / 256) * 256 < 65536;
 }
@@ -1202,47 +1189,6 @@ static int ensure_work(kpd_plan* p, const Dims& d, int k, hipStream_t st) {
   return KPD_OK;
 }
 
-// cbody_kernel arguments for features.(kCbFirst + 1)..12 of this pass, or
-// false when the coarse-body kernel does not apply (fp32 precision, an LDS
-// image that does not fit, KPD_NO_CBODY=1 for A/B runs).
-static bool cbody_setup(kpd_plan* p, const Dims& d, Work& w, const float* x, CbodyArgs& a) {
-  // opt-in (KPD_CBODY=1): measured slower than the batched path at C2
-  // (0.56 vs 0.27 ms for features.5..12 at 64 images: one CU per image leaves
-  // 3/4 of the chip idle and the per-image chain is latency-bound) and equal
-  // at C3 (body)
-  static const bool on = getenv("KPD_CBODY") != nullptr && atoi(getenv("KPD_CBODY")) != 0;
-  if (!on || p->precision == KPD_PRECISION_FP32 || !p->last.ws || !w.cbd) return false;
-  a = CbodyArgs{};
-  a.x = x;
-  a.nl = 11 - kCbFirst;
-  if (a.nl > kCbMaxLayers) return false;
-  for (int l = 0; l < a.nl; ++l) {
-    const int i = kCbFirst + l;
-    const DevBneck& bn = p->bn[i];
-    if (!bn.has_exp || !bn.cfg.se || !bn.expand.ws || !bn.project.ws) return false;
-    CbLayer& L = a.L[l];
-    L.Hi = d.h[i]; L.Wi = d.w[i]; L.Ho = d.h[i + 1]; L.Wo = d.w[i + 1];
-    L.k = bn.cfg.k; L.s = bn.cfg.s;
-    L.cin_p = pad16(bn.cfg.cin); L.kc_in = bn.expand.ws_kc;
-    L.Ep = bn.dw.Cp; L.EpK = (L.Ep + 31) / 32 * 32; L.C = bn.cfg.exp;
-    if (bn.project.ws_kc * 32 != L.EpK) return false;
-    L.cout_p = bn.project.cout_p; L.act = bn.cfg.act;
-    L.res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
-    L.se = 1; L.sq = bn.se.sq;
-    L.we = static_cast<const _Float16*>(bn.expand.ws); L.we_exp = bn.expand.w_exp; L.be = bn.expand.b;
-    L.wd = bn.dw.w; L.bd = bn.dw.b;
-    L.w1 = bn.se.w1; L.b1 = bn.se.b1; L.w2t = bn.se.w2; L.b2 = bn.se.b2;
-    L.wp = static_cast<const _Float16*>(bn.project.ws); L.wp_exp = bn.project.w_exp; L.bp = bn.project.b;
-    L.tap = i + 1 == 8 ? w.o[i] : nullptr;   // features.8 output: FPN tap 2
-  }
-  a.wl = static_cast<const _Float16*>(p->last.ws); a.wl_exp = p->last.w_exp; a.bl = p->last.b;
-  a.last_cin_p = p->last.cin_p; a.last_kc = p->last.ws_kc; a.last_cout = p->last.cout_p;
-  a.tap3 = w.last;
-  a.dscr = w.cbd;
-  a.dscr_floats = w.cbd_floats;
-  return cbody_lds_bytes(a) <= 160 * 1024;
-}
-
 // HeatmapHead (heatmap_head.py:81-151) on the [R][56][56][64] NHWC ROI
 // features in w.roi with their per-row statistics in w.roi_stats: channel
 // attention, spatial attention, the three 3x3 convs and the final 1x1 +
@@ -1260,7 +1206,7 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
   if (!(parts & KPD_HEAD_CHANNEL_ATT)) HIP_TRY(launch_fill(w.cw, (long)R * 64, 1.f, st));
   const bool bf = p->precision == KPD_PRECISION_MIXED;
   const int xs_mode = hsplit ? 3 : bf ? (hm_padded(p) ? 2 : 1) : 0;
-  static const bool att_2k = getenv("KPD_HM_ATT_2K") != nullptr;   // A/B: pool and apply as two launches
+  static const bool att_2k = kpd_diag_env("KPD_HM_ATT_2K") != nullptr;   // A/B: pool and apply as two launches
   if (att_2k) {
     HIP_TRY(launch_hm_spool(w.roi, w.cw, R, w.smap, st));
     HIP_TRY(launch_hm_sapply(w.roi, w.cw, w.smap, p->sa_w, p->sa_b, R, w.xs, xs_mode, st, w.hsc,
@@ -1285,7 +1231,7 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
   c2.reset();
   std::unique_ptr<Stage> c3(new Stage(p, "hm_conv3", st));
   // mixed / split: the final 1x1 + sigmoid runs in conv 3's epilogue (no h3 round trip)
-  static const bool no_fin_fuse = getenv("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
+  static const bool no_fin_fuse = kpd_diag_env("KPD_NO_FINAL_FUSE") != nullptr;   // A/B switch
   const bool fin_fused = (p->hm3.bf16 || p->hm3.ws) && p->hm3.cout_p == 64 && (!no_fin_fuse || p->hm3.ws);
   const HmFinal fin{p->fin_w, p->fin_b, w.slot, P, heat_out};
   if (int rc = hm_conv(p, p->hm3, w.h2, R, p->hm2.cout_p, w.h3, 2, st, fin_fused ? &fin : nullptr, stamps3, &sp3))
@@ -1308,7 +1254,7 @@ static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts,
     // intermediate by 6, the input by the FPN level-0 maximum.  The spatial
     // attention (1x1 convs + sigmoid + apply) is one kernel writing the first
     // conv's operand (KPD_KH_ATT1=1: the fp32 1x1 conv + apply kernel, A/B).
-    static const bool att1 = getenv("KPD_KH_ATT1") != nullptr;
+    static const bool att1 = kpd_diag_env("KPD_KH_ATT1") != nullptr;
     if (att1 || !p->kh_sa1.ws) {
       if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
         return rc;
@@ -1427,7 +1373,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
 
   // KPD_STAMPS: per-workgroup phase stamps of the SE-block kernels (debug
   // buffers "stamps_exdw_<i>" / "stamps_seproj_<i>", single-stream forwards)
-  static const bool want_stamps = getenv("KPD_STAMPS") != nullptr;
+  static const bool want_stamps = kpd_diag_env("KPD_STAMPS") != nullptr;
   constexpr size_t kStampWords = 1 << 20;
   if (want_stamps && !p->stamps) {
     HIP_TRY(hipMalloc(&p->stamps, kStampWords * 8));
@@ -1450,21 +1396,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   HIP_TRY(launch_stem(image, B, C, H, W, p->stem_w, p->stem_b, w.stem, d.h[0], d.w[0], lin ? w.sc : nullptr, st));
   const float* x = w.stem;
   const float* taps[4] = {w.stem, nullptr, nullptr, nullptr};
-  bool cb_done = false;
   for (int i = 0; i < 11; ++i) {
     const DevBneck& bn = p->bn[i];
     const int hi = d.h[i], wi = d.w[i], ho = d.h[i + 1], wo = d.w[i + 1];
-    // features.(kCbFirst + 1)..12 as one launch, a workgroup per image (cbody.hip)
-    CbodyArgs cba;
-    if (i == kCbFirst && cbody_setup(p, d, w, x, cba)) {
-      cba.stamps = take_stamps("stamps_cbody", (size_t)B * 16);
-      static const int cb_dbg = getenv("KPD_CBODY_DBG") ? atoi(getenv("KPD_CBODY_DBG")) : 0;   // ablations
-      cba.dbg = cb_dbg;
-      HIP_TRY(launch_cbody(cba, B, st));
-      taps[2] = w.o[7];
-      cb_done = true;
-      break;
-    }
     const int inp = pad16(bn.cfg.cin);
     // coarse maps: expand + depthwise (+ SE means) fused when the image fits LDS
     ExDwArgs xa{};
@@ -1474,15 +1408,15 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     xa.act_e = bn.cfg.act; xa.wd = bn.dw.w; xa.bd = bn.dw.b; xa.act_d = bn.dw.act; xa.Ep = bn.dw.Cp;
     xa.out = w.d[i]; xa.Ho = ho; xa.Wo = wo; xa.pooled = bn.cfg.se ? w.pool : nullptr;
     bool fused = false;
-    static const bool no_fuse = getenv("KPD_NO_FUSE") != nullptr;   // A/B switch for measurements
+    static const bool no_fuse = kpd_diag_env("KPD_NO_FUSE") != nullptr;   // A/B switch for measurements
     // no SE: the whole block (expand, depthwise, project, residual) in one kernel on row tiles
     // fused by default only at stride 2 (features.2: -31 us per step); the stride-1
     // block (features.3) measured 6 us slower fused than as three kernels.
     // KPD_FIR_MASK (bit i = block i) overrides for A/B runs.
-    static const int fir_mask = getenv("KPD_FIR_MASK") ? atoi(getenv("KPD_FIR_MASK")) : -1;
+    static const int fir_mask = kpd_diag_env("KPD_FIR_MASK") ? atoi(kpd_diag_env("KPD_FIR_MASK")) : -1;
     const bool fir_on = fir_mask < 0 ? bn.cfg.s == 2 : ((fir_mask >> i) & 1) != 0;
     // features.1: 16 channels, no expand, SE -> depthwise + tile sums, excitation + project
-    static const bool no_f1 = getenv("KPD_NO_F1") != nullptr;   // A/B switch
+    static const bool no_f1 = kpd_diag_env("KPD_NO_F1") != nullptr;   // A/B switch
     if (!no_f1 && !bn.has_exp && bn.cfg.se && bn.dw.Cp == 16 && bn.cfg.cout == 16 && bn.project.cout_p == 16 &&
         bn.project.cin_p == 16 && bn.project.k == 1 && !bn.project.bf16 && bn.se.sq <= 16 && bn.dw.k == 3 &&
         !(bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout) && 4 * ((wo + 3) / 4) * 4 <= 256) {
@@ -1517,20 +1451,20 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
         inp <= 96) {
       // slice width fixed per layer (never per batch: the fc1 partial sums
       // must not depend on what an image is batched with)
-      static const int cs_env = getenv("KPD_EXDW_CS") ? atoi(getenv("KPD_EXDW_CS")) : 0;   // A/B sweeps
+      static const int cs_env = kpd_diag_env("KPD_EXDW_CS") ? atoi(kpd_diag_env("KPD_EXDW_CS")) : 0;   // A/B sweeps
       // 32 channels from 288 expanded channels up, else 16 (48 for the
       // 576-wide blocks measured slower: 188 VGPRs, 30 vs 23 us)
       xa.CS = cs_env > 0 ? cs_env : (bn.dw.Cp >= 288 ? 32 : 16);
       // no SE and under two workgroups per CU: split the output rows in two
       // bands (features.3 at 64 images: 384 -> 768 workgroups)
-      static const int nband_env = getenv("KPD_EXDW_NBAND") ? atoi(getenv("KPD_EXDW_NBAND")) : 0;   // A/B
+      static const int nband_env = kpd_diag_env("KPD_EXDW_NBAND") ? atoi(kpd_diag_env("KPD_EXDW_NBAND")) : 0;   // A/B
       xa.nband = !bn.cfg.se && (long)(bn.dw.Cp / xa.CS) * B < 512 ? 2 : 1;
       if (nband_env > 0 && !bn.cfg.se) xa.nband = std::min(nband_env, ho);
       fused = bn.dw.Cp % xa.CS == 0 && exdw_lds_bytes(xa, bn.dw.k) <= 160 * 1024;
     }
     // SE blocks on the coarse maps: fc1 partials in exdw_kernel, then the
     // excitation + project (+ residual) in one seproj_kernel launch
-    static const bool no_seproj = getenv("KPD_NO_SEPROJ") != nullptr;   // A/B switch
+    static const bool no_seproj = kpd_diag_env("KPD_NO_SEPROJ") != nullptr;   // A/B switch
     const bool seproj = fused && bn.cfg.se && !no_seproj && bn.project.k == 1 && !bn.project.bf16 &&
                         bn.project.cin_p == bn.dw.Cp && bn.se.sq <= 144 && bn.se.C % 4 == 0 &&
                         (ho * wo == 48 || ho * wo == 192) && (size_t)(bn.dw.Cp / xa.CS) * bn.se.sq <= kSePartFloats;
@@ -1547,7 +1481,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       sa.part = w.separt; sa.nsl = bn.dw.Cp / xa.CS; sa.sq = bn.se.sq; sa.C = bn.se.C;
       sa.b1 = bn.se.b1; sa.w2t = bn.se.w2; sa.b2 = bn.se.b2;
       sa.wp = static_cast<const float*>(bn.project.w); sa.bp = bn.project.b; sa.cout_p = bn.project.cout_p;
-      static const int nt_env = getenv("KPD_SEPROJ_NT") ? atoi(getenv("KPD_SEPROJ_NT")) : 0;
+      static const int nt_env = kpd_diag_env("KPD_SEPROJ_NT") ? atoi(kpd_diag_env("KPD_SEPROJ_NT")) : 0;
       sa.NT = nt_env > 0 ? nt_env : (sa.Po == 48 ? 32 : 16);
       if (sa.cout_p % sa.NT) sa.NT = 16;
       const bool res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
@@ -1555,7 +1489,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       sa.out = w.o[i];
       // wide blocks (C >= 288): the excitation as its own launch (one fc2
       // pass per image instead of one per project workgroup)
-      static const int se_split_env = getenv("KPD_SE_SPLIT") ? atoi(getenv("KPD_SE_SPLIT")) : -1;   // A/B
+      static const int se_split_env = kpd_diag_env("KPD_SE_SPLIT") ? atoi(kpd_diag_env("KPD_SE_SPLIT")) : -1;   // A/B
       if (se_split_env == 1 || (se_split_env < 0 && bn.se.C >= 288)) {
         HIP_TRY(launch_se_excite(sa, B, w.sesc[i], st));
         sa.sesc = w.sesc[i];
@@ -1587,10 +1521,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     if (i + 1 == 3) taps[1] = x;
     if (i + 1 == 8) taps[2] = x;
   }
-  if (!cb_done)
-    if (int rc = conv(p->last, x, B, d.h[11], d.w[11], pad16(96), w.last, ACT_HSWISH, nullptr, 0, 0, nullptr,
-                      nullptr, 0, 0, st))
-      return rc;
+  if (int rc = conv(p->last, x, B, d.h[11], d.w[11], pad16(96), w.last, ACT_HSWISH, nullptr, 0, 0, nullptr,
+                    nullptr, 0, 0, st))
+    return rc;
   taps[3] = w.last;
   body_stage.reset();
   if (int rc = mark(1)) return rc;
@@ -1600,7 +1533,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   std::unique_ptr<Stage> lat_stage(new Stage(p, "fpn_lateral", st));
   // laterals 3 -> 1 in one launch (lateral_chain.hip) when only lateral 1 is
   // consumed (kpd_backbone returns every level: the per-level convs then)
-  static const bool no_chain = getenv("KPD_NO_LAT_CHAIN") != nullptr;   // A/B switch
+  static const bool no_chain = kpd_diag_env("KPD_NO_LAT_CHAIN") != nullptr;   // A/B switch
   LatChainArgs lc{};
   lc.t1 = taps[1]; lc.t2 = taps[2]; lc.t3 = taps[3];
   lc.L1 = static_cast<const float*>(p->lat[1].w); lc.L2 = static_cast<const float*>(p->lat[2].w);
@@ -1615,7 +1548,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   lc.lat1_split = lin ? reinterpret_cast<_Float16*>(reinterpret_cast<char*>(w.lat[0]) + (size_t)B * lh[0] * lw[0] * 64)
                       : nullptr;
   lc.amax = lin ? w.sc : nullptr;
-  static const bool no_chain_t0 = getenv("KPD_NO_CHAIN_TAP0") != nullptr;   // A/B: tap0 split as its own launch
+  static const bool no_chain_t0 = kpd_diag_env("KPD_NO_CHAIN_TAP0") != nullptr;   // A/B: tap0 split as its own launch
   if (lin && !no_chain_t0) {
     lc.t0 = taps[0];
     lc.t0_split = reinterpret_cast<_Float16*>(w.lat[0]);
@@ -1767,12 +1700,20 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
       (uintptr_t)image, (uintptr_t)B, (uintptr_t)C, (uintptr_t)H, (uintptr_t)W, (uintptr_t)boxes, (uintptr_t)NB,
       (uintptr_t)P, (uintptr_t)flags, (uintptr_t)kpts, (uintptr_t)vis, (uintptr_t)heat, (uintptr_t)kh_kpts,
       (uintptr_t)kh_vis, (uintptr_t)box_scores, (uintptr_t)topk_out, (uintptr_t)stream, (uintptr_t)p->streams};
+  auto eager = [&](void* s_) {
+    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
+                        topk_out, s_);
+  };
   if (p->graphs.size() >= 64 && !p->graphs.count(key)) {   // signatures that never repeat: bounded
+    // the executable graphs may still be running on their callers' streams
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipDeviceSynchronize());
     for (auto& kv : p->graphs)
       if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
     p->graphs.clear();
   }
   kpd_plan::GraphEntry& g = p->graphs[key];
+  if (g.never) return eager(stream);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (g.exec && g.epoch == p->ws_epoch) {
     HIP_TRY(hipSetDevice(p->device));
@@ -1787,36 +1728,63 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
     HIP_TRY(hipGraphLaunch(g.exec, st));
     return KPD_OK;
   }
-  if (g.exec) {
+  if (g.exec) {   // stale (re-carve, re-finalize, detector change): it may still be running
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipDeviceSynchronize());
     (void)hipGraphExecDestroy(g.exec);
     g.exec = nullptr;
     g.seen = 0;
   }
   if (g.seen++ == 0)   // eager: allocations and first-use setup happen outside any capture
-    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
-                        topk_out, stream);
+    return eager(stream);
   HIP_TRY(hipSetDevice(p->device));
   if (!p->graph_st) HIP_TRY(hipStreamCreateWithFlags(&p->graph_st, hipStreamNonBlocking));
-  if (!p->graph_ev) HIP_TRY(hipEventCreateWithFlags(&p->graph_ev, hipEventDisableTiming));
+  // The captured forward_impl updates host-side workspace state (sc_dirty,
+  // and on a re-carve have_work / dims) as if its work had run.  If the
+  // capture is abandoned, none of it ran: restore that state, so the eager
+  // retry zeroes what it must (a dirty split-scale slot, a re-carved
+  // workspace's zero borders).
+  bool dirty0[kpd_plan::kMaxSub + 1], have0[kpd_plan::kMaxSub + 1];
+  for (int k = 0; k <= kpd_plan::kMaxSub; ++k) {
+    dirty0[k] = p->work[k].sc_dirty;
+    have0[k] = p->have_work[k];
+  }
+  auto abandon = [&]() {
+    for (int k = 0; k <= kpd_plan::kMaxSub; ++k) {
+      p->work[k].sc_dirty = dirty0[k] || p->have_work[k] != have0[k];
+      // a slot (re-)carved inside the capture: its memset never ran -> carve again eagerly
+      if (p->have_work[k] && !have0[k]) p->have_work[k] = false;
+    }
+  };
   const long epoch0 = p->ws_epoch;
   HIP_TRY(hipStreamBeginCapture(p->graph_st, hipStreamCaptureModeRelaxed));
   const int rc = forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis,
                               box_scores, topk_out, p->graph_st);
   hipGraph_t graph = nullptr;
   const hipError_t ec = hipStreamEndCapture(p->graph_st, &graph);
-  if (rc != KPD_OK || ec != hipSuccess || p->ws_epoch != epoch0) {
+  const bool forced = p->graph_abandon_next;
+  p->graph_abandon_next = false;
+  if (rc != KPD_OK || ec != hipSuccess || p->ws_epoch != epoch0 || forced) {
     if (graph) (void)hipGraphDestroy(graph);
     (void)hipGetLastError();
     // not capturable here (an allocation or sync inside it, the carve changed
     // under it): this call runs eagerly and reports its own errors
+    abandon();
+    if (p->ws_epoch != epoch0)   // a re-carve inside the capture: every slot re-carves (and re-zeroes) eagerly
+      for (int k = 0; k <= kpd_plan::kMaxSub; ++k) p->have_work[k] = false;
     g.seen = 0;
-    return forward_impl(p, image, B, C, H, W, boxes, NB, P, flags, kpts, vis, heat, kh_kpts, kh_vis, box_scores,
-                        topk_out, stream);
+    return eager(stream);
   }
   hipGraphExec_t exec = nullptr;
   const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
-  HIP_TRY(ei);
+  if (ei != hipSuccess) {   // never capturable for this signature: eager from now on
+    (void)hipGetLastError();
+    abandon();
+    g.never = true;
+    g.seen = 0;
+    return eager(stream);
+  }
   g.exec = exec;
   g.epoch = p->ws_epoch;
   HIP_TRY(hipGraphLaunch(g.exec, st));
@@ -1877,8 +1845,8 @@ static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, in
   // that stage (1 body .. 5 ROI align) instead of starting at once;
   // KPD_PIPE_PRI=1 runs sub-batches 1.. on high-priority streams, so their
   // workgroups are dispatched ahead of the running sub-batch's at every free CU
-  static const int pipe_at = getenv("KPD_PIPE") ? atoi(getenv("KPD_PIPE")) : 0;
-  static const bool pipe_pri = getenv("KPD_PIPE_PRI") != nullptr;
+  static const int pipe_at = kpd_diag_env("KPD_PIPE") ? atoi(kpd_diag_env("KPD_PIPE")) : 0;
+  static const bool pipe_pri = kpd_diag_env("KPD_PIPE_PRI") != nullptr;
   if (!p->fork_ev) HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   for (int k = 1; k < S; ++k) {
     if (!p->sub_st[k]) HIP_TRY(hipStreamCreateWithFlags(&p->sub_st[k], hipStreamNonBlocking));
@@ -1916,7 +1884,9 @@ int kpd_plan_set_streams(kpd_plan* p, int n) {
 
 int kpd_plan_set_graphs(kpd_plan* p, int enable) {
   if (!p) return fail(KPD_EINVAL, "null plan");
+  if (enable < 0 || enable > 2) return fail(KPD_EINVAL, "enable must be 0, 1 or 2");
   p->use_graphs = enable != 0;
+  p->graph_abandon_next = enable == 2;
   return KPD_OK;
 }
 

@@ -28,7 +28,7 @@ PRECISIONS = {"fp32": KPD_PRECISION_FP32, "split": KPD_PRECISION_SPLIT, "mixed":
 EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_tensor",
            "kpd_plan_finalize", "kpd_plan_destroy", "kpd_forward", "kpd_debug_copy", "kpd_nms",
            "kpd_plan_timing", "kpd_plan_timing_stage", "kpd_plan_timing_query", "kpd_plan_set_detector",
-           "kpd_bench_conv16",
+           "kpd_bench_conv16", "kpd_build_flags",
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
            "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
            "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss", "kpd_conv3x3_forward",
@@ -46,7 +46,14 @@ class KpdNativeError(RuntimeError):
 
 
 def lib_path() -> Path:
-    return Path(os.environ.get("KPD_LIB", str(_LIB_PATH)))
+    """libkpd.so next to this package; KPD_LIB overrides the path, and
+    KPD_DIAG_LIB=1 selects the diagnostic build (make diag: libkpd_diag.so,
+    which reads the KPD_* A/B / ablation switches -- measurement tools only)."""
+    if "KPD_LIB" in os.environ:
+        return Path(os.environ["KPD_LIB"])
+    if os.environ.get("KPD_DIAG_LIB") == "1":
+        return _LIB_PATH.with_name("libkpd_diag.so")
+    return _LIB_PATH
 
 
 def load() -> ctypes.CDLL:
@@ -160,9 +167,12 @@ class Plan:
         """Sub-batch streams for large batches (kpd_plan_set_streams)."""
         check(self.lib.kpd_plan_set_streams(self.h, int(n)), "kpd_plan_set_streams")
 
-    def set_graphs(self, enable: bool) -> None:
-        """Replay repeated forwards as hipGraphs (kpd_plan_set_graphs)."""
-        check(self.lib.kpd_plan_set_graphs(self.h, 1 if enable else 0), "kpd_plan_set_graphs")
+    def set_graphs(self, enable: bool, abandon_next_capture: bool = False) -> None:
+        """Replay repeated forwards as hipGraphs (kpd_plan_set_graphs);
+        abandon_next_capture (tests) makes the next capture fail over to an
+        eager forward."""
+        mode = (2 if abandon_next_capture else 1) if enable else 0
+        check(self.lib.kpd_plan_set_graphs(self.h, mode), "kpd_plan_set_graphs")
 
     def forward(self, image: torch.Tensor, boxes: Optional[torch.Tensor], kpts, vis, heat, flags: int = 0,
                 kh_kpts=None, kh_vis=None, box_scores=None, topk=None) -> None:

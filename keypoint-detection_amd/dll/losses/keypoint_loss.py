@@ -19,9 +19,6 @@ from .. import _native
 class _AdaptiveHeatmapLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pred, gt, target_weight, kw, bw, adaptive, alpha):
-        if gt.requires_grad:
-            raise NotImplementedError("AdaptiveHeatmapLoss: the gradient with respect to gt_heatmaps is not "
-                                      "implemented (only d loss / d pred_heatmaps)")
         loss, grad, thr = _native.adaptive_heatmap_loss(pred, gt, target_weight, kw, bw, adaptive, alpha,
                                                         want_grad=pred.requires_grad)
         ctx.save_for_backward(grad if grad is not None else torch.empty(0, device=pred.device))
@@ -61,5 +58,9 @@ class AdaptiveHeatmapLoss(nn.Module):
 
     def forward(self, pred_heatmaps: torch.Tensor, gt_heatmaps: torch.Tensor,
                 target_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+        # (checked here: inside an autograd Function's forward grad mode is always off)
+        if torch.is_grad_enabled() and gt_heatmaps.requires_grad:
+            raise NotImplementedError("AdaptiveHeatmapLoss: the gradient with respect to gt_heatmaps is not "
+                                      "implemented (only d loss / d pred_heatmaps)")
         return _AdaptiveHeatmapLossFn.apply(pred_heatmaps, gt_heatmaps, target_weight, self.keypoint_weight,
                                             self.background_weight, self.adaptive_threshold, self.focal_alpha)

@@ -23,7 +23,8 @@ class Conv3x3Function(torch.autograd.Function):
     def forward(ctx, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return _native.conv3x3_forward(x, weight, bias)
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return _native.conv3x3_forward(x, weight, bias).to(x.dtype)   # computed in fp32, returned like F.conv2d
 
     @staticmethod
     def backward(ctx, grad_y: torch.Tensor):
@@ -34,6 +35,8 @@ class Conv3x3Function(torch.autograd.Function):
             gw = gw.to(weight.dtype)
         if gx is not None:
             gx = gx.to(x.dtype)
+        if gb is not None:
+            gb = gb.to(ctx.bias_dtype)
         return gx, gw, gb
 
 

@@ -49,7 +49,7 @@ def main(argv=None):
     ap.add_argument("--split", default="val")
     ap.add_argument("--batch-size", type=int, default=32)
     ap.add_argument("--device", default="cuda")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "mixed"])
+    ap.add_argument("--precision", default="split", choices=["split", "fp32", "mixed"])
     args = ap.parse_args(argv)
     setup_logging()
     cfg = load_config(args.config)

@@ -11,7 +11,14 @@ Differences (documented in DESIGN.md):
     in this image; Resize/ToTensor/Normalize are bit-exact to Pillow;
   * ``--model synthetic`` builds the seeded synthetic weights (no trained
     checkpoint exists: the reference's outputs/best_model.pth is a missing blob);
-  * ``--size HxW`` allows the non-square 256x192 input of BASELINE config C1.
+  * ``--size HxW`` allows the non-square 256x192 input of BASELINE config C1;
+  * ``--precision`` picks the numeric mode; the default is ``split``, the
+    fp32-accurate headline path (f16 hi/lo x3 MFMA products), like the model's;
+  * without ``--gt`` the reference passes ``bboxes=None`` (:99), which makes its
+    model return all-zero keypoints (keypoint_model.py:111-113,123-135).  Here
+    the person detector supplies the boxes instead (the
+    build-defined glue of PERSON_HEAD + NMS, keypoint_model.py:114-119,
+    person_head.py:96-139); ``--reference-zeros`` keeps the reference's zeros.
 Runs on the HIP device (the accelerated path has no CPU fallback).
 """
 from __future__ import annotations
@@ -45,7 +52,7 @@ def setup_logging():
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
 
 
-def load_model(model_path, config_dict, device, precision="fp32"):
+def load_model(model_path, config_dict, device, precision="split"):
     """Reference load_model (:30-62): configs from the YAML, filtered
     strict=False state-dict load (weights_only -- nothing executable is
     unpickled)."""
@@ -85,12 +92,27 @@ def read_gt_boxes(gt_path, device):
     return torch.tensor(boxes, device=device)
 
 
-def predict_single_image(model, image_path, transform, device, gt_path=None, output_path=None):
+def predict_single_image(model, image_path, transform, device, gt_path=None, output_path=None,
+                         reference_zeros=False, return_outputs=False):
+    """Reference predict_single_image (:64-131).  Without a GT file the
+    detector branch runs (``model({'image': x})``: no 'bboxes' key), unless
+    ``reference_zeros`` asks for the reference's ``bboxes=None`` call."""
     from PIL import Image
     x = transform(Image.open(image_path).convert("RGB")).unsqueeze(0).to(device)
     bboxes = read_gt_boxes(gt_path, device) if gt_path and Path(gt_path).exists() else None
+    if bboxes is not None:
+        batch, mode = {"image": x, "bboxes": bboxes.unsqueeze(0)}, "given boxes"
+    elif reference_zeros:
+        batch, mode = {"image": x, "bboxes": None}, "reference zeros (bboxes=None)"
+    else:
+        batch, mode = {"image": x}, "person detector"
+    logging.info(f"{Path(image_path).name}: boxes from {mode}")
     with torch.no_grad():
-        outputs = model({"image": x, "bboxes": bboxes.unsqueeze(0) if bboxes is not None else None})
+        outputs = model(batch)
+    if bboxes is None and not reference_zeros:
+        n = int((outputs["box_scores"][0] > 0).sum())
+        logging.info(f"detector kept {n} person(s); person 0 box (cx, cy, w, h) = "
+                     f"{[round(float(v), 4) for v in outputs['boxes'][0][0]]}")
     keypoints = outputs["keypoints"].squeeze().cpu().numpy()
     print("\nPredicted Keypoints:")
     print("-" * 40)
@@ -101,7 +123,7 @@ def predict_single_image(model, image_path, transform, device, gt_path=None, out
         if i < len(keypoints):
             x_, y_ = keypoints[i]
             print(f"{i + 1:2d}. {name:<15} ({x_:.3f}, {y_:.3f})")
-    return keypoints
+    return (keypoints, outputs) if return_outputs else keypoints
 
 
 def main(argv=None):
@@ -112,7 +134,11 @@ def main(argv=None):
     ap.add_argument("--gt")
     ap.add_argument("--output", required=True)
     ap.add_argument("--device", default="cuda")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "mixed"])
+    ap.add_argument("--precision", default="split", choices=["split", "fp32", "mixed"],
+                    help="split (default): fp32-accurate f16x3 MFMA; fp32: fp32 MFMA; mixed: bf16 heatmap convs")
+    ap.add_argument("--reference-zeros", action="store_true",
+                    help="without --gt, call the model with bboxes=None like the reference (all-zero keypoints) "
+                         "instead of running the person detector")
     ap.add_argument("--size", default=None, help="HxW input size (default: input_size square)")
     args = ap.parse_args(argv)
     setup_logging()
@@ -126,13 +152,19 @@ def main(argv=None):
     inp = Path(args.input)
     gt = Path(args.gt) if args.gt else None
     Path(args.output).mkdir(parents=True, exist_ok=True)
+    logging.info(f"precision {args.precision}")
+    results = []
     if inp.is_file():
-        predict_single_image(model, inp, transform, device, gt if gt and gt.is_file() else None)
+        results.append((inp, predict_single_image(model, inp, transform, device, gt if gt and gt.is_file() else None,
+                                                  reference_zeros=args.reference_zeros, return_outputs=True)[1]))
     else:
         for img in sorted(inp.glob("*.*")):
             if img.suffix.lower() in (".jpg", ".jpeg", ".png"):
-                predict_single_image(model, img, transform, device, (gt / f"{img.stem}.txt") if gt else None)
+                out = predict_single_image(model, img, transform, device, (gt / f"{img.stem}.txt") if gt else None,
+                                           reference_zeros=args.reference_zeros, return_outputs=True)[1]
+                results.append((img, out))
     logging.info("Prediction completed successfully!")
+    return {"model": model, "results": results}
 
 
 if __name__ == "__main__":

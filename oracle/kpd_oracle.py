@@ -367,10 +367,11 @@ def forward(sd: SD, batch, return_debug: bool = False, dual_head: bool = False, 
     feat0 = backbone_level0(x, sd)
     feats, topk = select_top_k(feat0, sd)
     boxes = normalize_bboxes(batch, B)
+    det_s = None
     if boxes is None:
         if detect is None:
             raise NotImplementedError("person-detector branch: pass detect=dict(...)")
-        det, _ = person_detect(feat0, sd, x.shape[2], x.shape[3], **detect)
+        det, det_s = person_detect(feat0, sd, x.shape[2], x.shape[3], **detect)
         boxes = [det[b] for b in range(B)]
     K = NUM_KEYPOINTS
     if not boxes or all(len(b) == 0 for b in boxes):
@@ -409,6 +410,8 @@ def forward(sd: SD, batch, return_debug: bool = False, dual_head: bool = False, 
     if dual_head:
         out["kh_keypoints"] = torch.stack(pkk)
         out["kh_visibilities"] = torch.stack(pkv)
+    if det_s is not None:
+        out["box_scores"] = det_s
     if return_debug:
         out["_feat0"] = feat0; out["_topk"] = topk
     return out

@@ -78,3 +78,27 @@ def test_anchors_match_oracle():
     from oracle import kpd_oracle as O
     ph = PERSON_HEAD(PersonDetectionConfig())
     assert torch.equal(ph.anchors, O.generate_anchors())
+
+
+def test_default_build_reads_no_diagnostic_switches(monkeypatch):
+    """The production libkpd.so is not a diagnostic build: the ablation /
+    A/B switches (KPD_HMCONV_DBG=1 gives wrong results by design in a
+    `make diag` build) and the KPD_STAMPS phase stamps are compiled out, so
+    no environment variable other than KPD_GRAPH (the graph-replay default)
+    is ever read -- a stray KPD_HMCONV_DBG=1 on a serving box changes nothing."""
+    from dll import _native
+    monkeypatch.delenv("KPD_LIB", raising=False)
+    monkeypatch.delenv("KPD_DIAG_LIB", raising=False)
+    path = _native.lib_path()
+    assert path.name == "libkpd.so"
+    lib = _native.load()
+    assert lib.kpd_build_flags() & 1 == 0
+    switches = set()
+    for f in (ROOT / "keypoint-detection_amd" / "csrc").glob("*.hip"):
+        switches |= set(re.findall(r'kpd_diag_env\("(KPD_[A-Z0-9_]+)"\)', f.read_text()))
+    assert {"KPD_HMCONV_DBG", "KPD_FPN0X_DBG", "KPD_STAMPS"} <= switches
+    blob = path.read_bytes()
+    assert [n for n in sorted(switches) if n.encode() in blob] == []
+    assert b"KPD_GRAPH" in blob
+    monkeypatch.setenv("KPD_DIAG_LIB", "1")
+    assert _native.lib_path().name == "libkpd_diag.so"

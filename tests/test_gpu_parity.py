@@ -270,44 +270,144 @@ def test_dual_head_vs_oracle():
     np.testing.assert_allclose(out["kh_visibilities"].cpu().numpy(), ref["kh_visibilities"].numpy(), atol=1e-5)
 
 
-def test_person_detector_glue_vs_oracle():
+def _check_detections(got_boxes, got_scores, ref_boxes, ref_scores, what):
+    """Detected boxes / scores vs the oracle: identical keep sets (the same
+    number of kept persons per image, in the same slots), scores to 1e-5,
+    boxes to 1e-4."""
+    kept_got = (got_scores > 0).sum(dim=1)
+    kept_ref = (ref_scores > 0).sum(dim=1)
+    assert torch.equal(kept_got, kept_ref), f"{what}: kept counts {kept_got.tolist()} vs {kept_ref.tolist()}"
+    np.testing.assert_allclose(got_scores.numpy(), ref_scores.numpy(), atol=1e-5, err_msg=what)
+    np.testing.assert_allclose(got_boxes.numpy(), ref_boxes.numpy(), atol=1e-4, err_msg=what)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "split", "mixed"])
+def test_person_detector_glue_vs_oracle(precision):
     """No 'bboxes' -> build-defined detector glue (§8 a10): pooled 1x1 heads,
-    anchor decode, threshold, NMS (max 5).  Checked against the oracle on the
-    same FPN features, then the keypoint stage on the detected boxes."""
+    anchor decode, threshold, NMS (max 5).  At BASELINE C3's size (B = 256,
+    256x192, two sub-batch streams) in every precision, with a dynamic-range
+    outlier in the batch.  Nine images are checked twice against the oracle:
+    on the GPU's own FPN level 0 (isolates the glue) and on the oracle's FPN
+    level 0 computed from the image (the whole detector path, so a split-mode
+    level-0 error that moved a threshold or NMS decision fails here), then
+    the keypoint stage on the detected boxes."""
     from dll.models.synthetic import synthetic_images
-    m, sd = _dual_model()
-    img = synthetic_images(3, 3, 256, 192, seed=51)
+    m, sd = _dual_model(precision)
+    m.streams = 2
+    B = 256
+    img = synthetic_images(B, 3, 256, 192, seed=51, device=DEV)
+    img[17] *= 4.0                             # dynamic-range outlier (x25 saturates the
+    #                                            class sigmoids into exact ties, whose NMS
+    #                                            order the reference's unstable sort leaves open)
     with torch.no_grad():
-        out = m(img.to(DEV))          # plain tensor input: the reference's detector branch
-    feat = _nchw_feat(m.native_plan(DEV), 3, 128, 96)
+        out = m(img)                           # plain tensor input: the reference's detector branch
+    sel = [0, 1, 17, 63, 64, 127, 128, 200, 255]
+    feat = m.native_plan(DEV).debug_buffer("feat0").view(B, 128, 96, 128)[sel].permute(0, 3, 1, 2).cpu()
+    got = torch.stack([out["boxes"][i].cpu() for i in sel])
+    got_s = out["box_scores"][sel].cpu()
+    assert got.shape == (len(sel), 5, 4)
+    assert (got_s > 0).any(), "no person detected in the checked images"
     ref_boxes, ref_scores = O.person_detect(feat, sd, 256, 192, 0.3, 0.3, 5)
-    got = torch.stack([b.cpu() for b in out["boxes"]])
-    assert got.shape == (3, 5, 4)
-    np.testing.assert_allclose(out["box_scores"].cpu().numpy(), ref_scores.numpy(), atol=1e-5)
-    np.testing.assert_allclose(got.numpy(), ref_boxes.numpy(), atol=1e-4)
-    ref = O.forward(sd, {"image": img, "bboxes": got}, dual_head=True)
-    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
-    assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
-    np.testing.assert_allclose(out["kh_keypoints"].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=1e-5)
+    _check_detections(got, got_s, ref_boxes, ref_scores, "glue on the GPU's level 0")
+    img_c = img[sel].cpu()
+    feat_o = O.backbone_level0(img_c, sd)
+    ob, os_ = O.person_detect(feat_o, sd, 256, 192, 0.3, 0.3, 5)
+    _check_detections(got, got_s, ob, os_, "detector on the oracle's level 0")
+    ref = O.forward(sd, {"image": img_c, "bboxes": got}, dual_head=True)
+    tol = 1e-5 if precision != "mixed" else 1e-3
+    np.testing.assert_allclose(out["keypoints"][sel].cpu().numpy(), ref["keypoints"].numpy(), atol=tol)
+    if precision != "mixed":
+        assert torch.equal(out["visibilities"][sel].cpu(), ref["visibilities"])
+    np.testing.assert_allclose(out["kh_keypoints"][sel].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol)
 
 
-def test_predict_cli(tmp_path, capsys):
-    """scripts/predict.py end to end: YAML config (grayscale 224), synthetic
-    weights, a PNG and a YOLO label; printout format of the reference."""
+def _predict_module():
     import sys
-    from PIL import Image
     from conftest import PKG
-    sys.path.insert(0, str(PKG / "scripts"))
+    if str(PKG / "scripts") not in sys.path:
+        sys.path.insert(0, str(PKG / "scripts"))
     import predict
+    return predict, PKG
+
+
+def _cli_image(tmp_path):
+    from PIL import Image
     rng = np.random.default_rng(0)
     Image.fromarray(rng.integers(0, 255, (240, 180, 3), dtype=np.uint8)).save(tmp_path / "img.png")
+    return tmp_path / "img.png"
+
+
+@pytest.mark.parametrize("size", [None, "256x192"])
+def test_predict_cli(tmp_path, capsys, size):
+    """scripts/predict.py end to end at its default precision (split): YAML
+    config (grayscale 224, or 256x192 as in BASELINE C1), synthetic weights, a
+    PNG and a YOLO label; printout format of the reference.  The printed
+    person-0 keypoints are checked against the oracle's forward on the same
+    preprocessed image and boxes."""
+    predict, PKG = _predict_module()
+    png = _cli_image(tmp_path)
     (tmp_path / "img.txt").write_text("0 0.5 0.5 0.4 0.8\n0 0.3 0.4 0.2 0.3\n")
-    predict.main(["--config", str(PKG / "configs" / "default_config.yaml"), "--model", "synthetic",
-                  "--input", str(tmp_path / "img.png"), "--gt", str(tmp_path / "img.txt"),
-                  "--output", str(tmp_path / "out")])
+    args = ["--config", str(PKG / "configs" / "default_config.yaml"), "--model", "synthetic",
+            "--input", str(png), "--gt", str(tmp_path / "img.txt"), "--output", str(tmp_path / "out")]
+    if size:
+        args += ["--size", size]
+    res = predict.main(args)
     txt = capsys.readouterr().out
     assert "Keypoints shape: (2, 17, 2)" in txt
     assert " 1. nose" in txt and "17. right_ankle" in txt
+    model = res["model"]
+    assert model.precision == "split"
+    H, W = (256, 192) if size else (224, 224)
+    transform = predict.make_transform(1, (H, W), DEV)
+    from PIL import Image
+    x = transform(Image.open(png).convert("RGB")).unsqueeze(0).cpu()
+    sd = {k: v.cpu() for k, v in model.state_dict().items()}
+    boxes = torch.tensor([[[0.5, 0.5, 0.4, 0.8], [0.3, 0.4, 0.2, 0.3]]])
+    ref = O.forward(sd, {"image": x, "bboxes": boxes})
+    out = res["results"][0][1]
+    np.testing.assert_allclose(out["keypoints"].cpu().numpy(), ref["keypoints"].numpy(), atol=1e-5)
+    assert torch.equal(out["visibilities"].cpu(), ref["visibilities"])
+    k0 = ref["keypoints"][0, 0, 0]
+    assert f" 1. {'nose':<15} ({float(k0[0, 0]):.3f}, {float(k0[0, 1]):.3f})" in txt
+
+
+def test_predict_cli_detector(tmp_path, capsys, caplog):
+    """predict.py without --gt: the reference passes
+    bboxes=None and prints zeros (scripts/predict.py:99); here the person
+    detector supplies the boxes by default.  The detected boxes equal the
+    oracle's detector on the same FPN level 0, the printout shows person 0's
+    keypoints, and --reference-zeros restores the reference's all-zero output."""
+    import logging
+    predict, PKG = _predict_module()
+    png = _cli_image(tmp_path)
+    base = ["--config", str(PKG / "configs" / "default_config.yaml"), "--model", "synthetic",
+            "--input", str(png), "--output", str(tmp_path / "out"), "--size", "256x192"]
+    with caplog.at_level(logging.INFO):
+        res = predict.main(base)
+    txt = capsys.readouterr().out
+    assert "boxes from person detector" in caplog.text
+    model = res["model"]
+    out = res["results"][0][1]
+    assert out["keypoints"].shape == (1, 5, 1, 17, 2)
+    assert "Keypoints shape: (5, 17, 2)" in txt
+    feat = model.native_plan(DEV).debug_buffer("feat0").view(1, 128, 96, 128).permute(0, 3, 1, 2).cpu()
+    sd = {k: v.cpu() for k, v in model.state_dict().items()}
+    ref_boxes, ref_scores = O.person_detect(feat, sd, 256, 192, 0.3, 0.3, 5)
+    _check_detections(torch.stack([b.cpu() for b in out["boxes"]]), out["box_scores"].cpu(), ref_boxes, ref_scores,
+                      "predict.py detector")
+    kept = int((ref_scores > 0).sum())
+    if kept:
+        k0 = out["keypoints"][0, 0, 0].cpu()
+        assert k0.abs().sum() > 0
+        assert f" 1. {'nose':<15} ({float(k0[0, 0]):.3f}, {float(k0[0, 1]):.3f})" in txt
+    caplog.clear()
+    with caplog.at_level(logging.INFO):
+        res = predict.main(base + ["--reference-zeros"])
+    txt = capsys.readouterr().out
+    assert "reference zeros" in caplog.text
+    out = res["results"][0][1]
+    assert not out["keypoints"].any() and out["keypoints"].shape == (1, 1, 17, 2)
+    assert " 1. nose            (0.000, 0.000)" in txt
 
 
 @pytest.mark.parametrize("precision", ["fp32", "split", "mixed"])
@@ -380,6 +480,46 @@ def test_graph_replay_matches_eager(model_sd, streams):
             torch.cuda.synchronize()
             assert torch.equal(kpts, ref2["keypoints"]) and torch.equal(heat, ref2["heatmap"]), it
             assert torch.equal(vis, ref2["visibilities"]), it
+    finally:
+        plan.set_graphs(False)
+
+
+def test_graph_capture_failure_recovers(model_sd):
+    """An abandoned capture (kpd_plan_set_graphs mode 2 forces it) runs the
+    call eagerly with the plan's workspace state restored: the captured
+    forward had marked the split-scale slots clean and may have re-carved,
+    but none of its work ran.  Outputs stay bit-identical to eager through the
+    failed capture, a re-carve, the next (successful) capture and replays."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m = _model(model_sd, "split")
+    B, P = 16, 2
+    img = synthetic_images(B, 3, 256, 192, seed=91, device=DEV)
+    boxes = synthetic_boxes(B, P, seed=92, device=DEV)
+    with torch.no_grad():
+        ref = m({"image": img, "bboxes": boxes})
+    plan = m.native_plan(DEV)
+    kpts = torch.empty(B, P, 1, 17, 2, device=DEV)
+    vis = torch.empty(B, P, 1, 17, 3, device=DEV)
+    heat = torch.empty(B, P, 17, 56, 56, device=DEV)
+    try:
+        for it, mode in enumerate((True, "abandon", None, None, "grow", None, None, None)):
+            if mode == "abandon":
+                plan.set_graphs(True, abandon_next_capture=True)
+            if mode == "grow":   # a larger batch re-carves the workspace (stale graphs, fresh zero borders)
+                big = synthetic_images(2 * B, 3, 256, 192, seed=93, device=DEV)
+                with torch.no_grad():
+                    m({"image": big, "bboxes": torch.cat([boxes, boxes])})
+                plan.set_graphs(True, abandon_next_capture=True)
+            elif mode is True:
+                plan.set_graphs(True)
+            kpts.fill_(-1.0)
+            heat.fill_(-1.0)
+            vis.fill_(-1.0)
+            plan.forward(img, boxes, kpts, vis, heat)
+            torch.cuda.synchronize()
+            assert torch.equal(kpts, ref["keypoints"]), it
+            assert torch.equal(heat, ref["heatmap"]), it
+            assert torch.equal(vis, ref["visibilities"]), it
     finally:
         plan.set_graphs(False)
 

@@ -101,29 +101,9 @@ def c1_latency(m, c, precision):
             "max_abs_dkpt_vs_cpu": float((out["keypoints"].cpu() - ref["keypoints"]).abs().max())}
 
 
-def kh_flops_per_roi(c=128, fine=64, reg=32, vis=32, h=56, w=56):
-    """KEYPOINT_HEAD algorithmic flops per ROI (keypoint_head.py:9-90): 2*MAC
-    of its convs and linears at the ROI resolution (BN folded)."""
-    hw = h * w
-    f = 2.0 * hw * (c * (c // 2) + (c // 2))                        # spatial attention 1x1 C->C/2->1
-    f += 2.0 * hw * (c * fine * 9 + (c * fine if c != fine else 0))  # ResidualBlock(C->64) (+ downsample)
-    f += 2.0 * hw * (fine * reg * 9 + (fine * reg if fine != reg else 0))
-    f += 2.0 * hw * reg * (reg // 2) * 9                               # 3x3 32->16
-    f += 2.0 * ((reg // 2) * (h // 4) * (w // 4) * 256 + 256 * 34)    # regression linears
-    f += 2.0 * hw * c * vis * 9 + 2.0 * (vis * 16 * 128 + 128 * 51)   # visibility branch
-    return f
-
-
 def config_flops(H, W, P, detect):
-    """Per-image algorithmic flops of a C3 / C5 forward: backbone
-    + FPN level 0 + P x (heatmap head + KEYPOINT_HEAD) (+ the detector's 1x1
-    heads on the 56x56-pooled 128-channel level 0)."""
     import bench
-    fl = dict(bench.flops_per_image(H, W, P))
-    kh = kh_flops_per_roi()
-    fl["keypoint_head"] = P * kh
-    fl["total"] += P * kh + (2.0 * 3136 * 128 * 45 if detect else 0.0)
-    return fl
+    return bench.config_flops(H, W, P, detect)
 
 
 def stage_breakdown(m, batch, iters=1):
@@ -166,36 +146,31 @@ def dominant_timed(m, batch, stage, steps):
     return (ms / n if n else None), n
 
 
-def cpu_sample(sd, img, boxes, detect, threads, runs=3):
-    """The oracle on a bounded sample: dual head, and for C3 the detector glue
+def cpu_sample(sd, img, boxes, detect, threads):
+    """The oracle on a bounded sample (bench.cpu_baseline's protocol: 3
+    warm-ups + median of >= 5): dual head, and for C3 the detector glue
     (oracle person_detect on the oracle's own FPN level 0) before the heads."""
+    import bench
     from oracle import kpd_oracle as O
-    torch.set_num_threads(threads)
 
     def fwd():
         if detect:
             return O.forward(sd, {"image": img}, dual_head=True,
                              detect=dict(conf_threshold=0.3, iou_threshold=0.3, max_persons=5))
         return O.forward(sd, {"image": img, "bboxes": boxes}, dual_head=True)
-
-    out = fwd()
-    ts = []
-    for _ in range(runs):
-        t0 = time.perf_counter()
-        fwd()
-        ts.append(time.perf_counter() - t0)
-    ts.sort()
-    return out, img.shape[0] / ts[len(ts) // 2], ts
+    return bench.cpu_baseline(sd, img, boxes, threads, fwd=fwd)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--cpu-sample", type=int, default=4, help="images in the C3 / C5 CPU-baseline sample (0 = none)")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="images in the C3 / C5 CPU-baseline sample (0 = none)")
     ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"])
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--configs", default="C1,C3,C5")
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r04" / "pmc.json"),
+                    help="rocprofv3 --pmc summary (tools/prof_stages.py --tag <config>) for roofline.traffic")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -241,7 +216,8 @@ def main():
         nl = bd[dom][1]
         stages = {k: v[0] for k, v in bd.items()}
         stages[dom] = dms
-        roof = bench.roofline(a.precision, stages, fl, c["B"] / nl, c["H"], c["W"], None, dom)
+        pmc = json.loads(Path(a.pmc_json).read_text()) if Path(a.pmc_json).exists() else None
+        roof = bench.roofline(a.precision, stages, fl, c["B"] / nl, c["H"], c["W"], pmc, dom, tag=name)
         roof["launches_timed"] = dn
         roof["images_per_launch"] = c["B"] / nl
         roof["timing"] = "HIP events around every launch of this stage in single-stream forwards after the warm-up"
@@ -253,13 +229,13 @@ def main():
             ci = bench.host_cpu_info()
             S = min(a.cpu_sample, c["B"])
             sd = {k: v.cpu() for k, v in m.state_dict().items()}
-            ref, rate, ts = cpu_sample(sd, img[:S].cpu(), batch["bboxes"][:S].cpu() if c["P"] else None, detect,
-                                       ci["threads"])
+            ref, rate, proto = cpu_sample(sd, img[:S].cpu(), batch["bboxes"][:S].cpu() if c["P"] else None, detect,
+                                          ci["threads"])
             line["cpu_baseline"] = {
                 "value": round(rate, 3), "unit": "images/s", "cores": ci["threads"], "kind": "port",
                 "sample": f"{S} images of the same {name} workload, oracle/kpd_oracle.py (dual head"
-                          f"{', detector glue' if detect else ''}), 1 warmup + median of {len(ts)} runs",
-                "cpu_model": ci["model"]}
+                          f"{', detector glue' if detect else ''}), {proto['warmups']} warmups + median of "
+                          f"{proto['runs']} runs", "protocol": proto, "cpu_model": ci["model"]}
             line["gpu_vs_cpu"] = round(line["images_per_s"] / rate, 1)
             gk = out["keypoints"][:S].cpu()
             line["parity"] = {"max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),

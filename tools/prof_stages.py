@@ -79,10 +79,14 @@ def main():
     ap.add_argument("--skip", type=int, default=2)
     ap.add_argument("--take", type=int, default=0, help="forwards kept after --skip (0 = all): the bench's timed region")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tag", default=None, help="config tag appended to the stage keys ('<stage>:<precision>@<tag>', "
+                                                "e.g. C3): the key bench.py reads for that config's roofline")
     a = ap.parse_args()
     # repo-relative source path (the GPU box's scratch root differs per call)
     src = os.path.relpath(os.path.abspath(a.outdir), os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))
-    res = {"_meta": {"source": src, "precision": a.precision, "skip_forwards": a.skip, "take_forwards": a.take}}
+    res = {"_meta": {"source": src, "precision": a.precision, "skip_forwards": a.skip, "take_forwards": a.take,
+                     "tag": a.tag}}
+    pk = a.precision + (f"@{a.tag}" if a.tag else "")     # the key suffix of the stage entries
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from bench import kernel_src_hash
@@ -111,7 +115,7 @@ def main():
         res["_meta"]["forwards_traced"] = len(fw)
         res["_meta"]["forward_kernel_us"] = round(sum(sum(v) for v in kn.values()) / max(len(fw), 1), 2)
         for lab, v in st.items():
-            res[f"{lab}:{a.precision}"] = {"avg_us": round(sum(v) / len(v), 3), "min_us": round(min(v), 3),
+            res[f"{lab}:{pk}"] = {"avg_us": round(sum(v) / len(v), 3), "min_us": round(min(v), 3),
                                            "max_us": round(max(v), 3), "launches": len(v),
                                            "src_hash": res["_meta"]["src_hash"]}
         res["kernels_us"] = {k: {"avg_us": round(sum(v) / len(v), 3), "calls": len(v),
@@ -145,7 +149,7 @@ def main():
                         agg[name][c].append(v)
                 for lab, cs in per.items():
                     for c, v in cs.items():
-                        agg[f"{lab}:{a.precision}"][c].append(v)
+                        agg[f"{lab}:{pk}"][c].append(v)
         for k, cs in agg.items():
             e = res.setdefault(k, {}) if ":" in k else res.setdefault("counters", {}).setdefault(k, {})
             for c, v in cs.items():
