@@ -72,6 +72,12 @@ void kpd_plan_destroy(kpd_plan* plan);
 
 #define KPD_FLAG_DETECT 1     /* no caller boxes: person detector + NMS WRITE boxes [B][P][4] */
 #define KPD_FLAG_DUAL_HEAD 2  /* also run KEYPOINT_HEAD on 128-ch ROI features */
+/* Write every pixel of FPN level 0.  By default, with caller boxes, the
+ * level-0 conv stores only the pixels the ROI aligns of the image's boxes
+ * read (the channel statistics of the top-k still see every pixel), and
+ * kpd_debug_copy has no "feat0"; this flag stores the whole map (inspection,
+ * tests).  Outputs are identical either way. */
+#define KPD_FLAG_FULL_LEVEL0 4
 
 /* Full eval forward.
  *   image:  [B][C][H][W] fp32 (NCHW, as the reference receives it), device

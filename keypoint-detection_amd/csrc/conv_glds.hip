@@ -584,7 +584,8 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int STAGE = (BM + BN) * ROWB, RING = S * STAGE;
   // ring | stats exchange [2][WAVES_M][BN] | bias [BN] | class tables (ng, woff, g[4]) x 16
   constexpr int SMISC = RING + 2 * WAVES_M * BN * 4;
-  constexpr int LDS = SMISC + BN * 4 + 16 * 6 * 4 + kFpn0xMaxImg * 4;   // + per-image unscale
+  // + per-image unscale + per-image store rectangle (x0 | x1 << 16, y0 | y1 << 16)
+  constexpr int LDS = SMISC + BN * 4 + 16 * 6 * 4 + kFpn0xMaxImg * 4 + kFpn0xMaxImg * 8;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   constexpr int KT0 = 5;                          // tap0 K-tiles: taps (2k, 2k+1)
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
@@ -638,6 +639,33 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     fpn0x_exps(p.sc[(size_t)u * kAmaxStride], p.sc[(size_t)(p.sc_n + u) * kAmaxStride], p.w_exp0, p.w_expE, &a_f,
                &a_l, &P);
     s_unscale[u] = ldexpf(1.f, -P);
+  }
+  // store rectangle of image u: every pixel roi_align (keypoint_model.py:
+  // 212-228; the same corner / extent formulas as roi_row_sample) can read
+  // for one of the image's boxes -- rows floor(y1) .. floor(y1 + roi_h) + 1
+  // (+ one pixel of margin each side) -- or the whole map without boxes
+  int2* s_fp = reinterpret_cast<int2*>(lds + SMISC + BN * 4 + 16 * 6 * 4 + kFpn0xMaxImg * 4);
+  for (int u = tid; u < p.N; u += NT) {
+    int x0 = 0, x1 = Wf - 1, y0 = 0, y1 = Hf - 1;
+    if (p.fp_boxes) {
+      x0 = y0 = 1 << 15;
+      x1 = y1 = -1;
+      for (int q = 0; u < p.fp_NB && q < p.fp_P; ++q) {
+        const float* bx = p.fp_boxes + ((size_t)u * p.fp_P + q) * 4;
+        const float cx = bx[0], cy = bx[1], bw = bx[2], bh = bx[3];
+        if (cx == 0.f && cy == 0.f && bw == 0.f && bh == 0.f) continue;   // skipped box (keypoint_model.py:149-153)
+        const float fx1 = fminf(fmaxf(cx - bw / 2.f, 0.f), 1.f) * (float)Wf;
+        const float fy1 = fminf(fmaxf(cy - bh / 2.f, 0.f), 1.f) * (float)Hf;
+        const float fx2 = fminf(fmaxf(cx + bw / 2.f, 0.f), 1.f) * (float)Wf;
+        const float fy2 = fminf(fmaxf(cy + bh / 2.f, 0.f), 1.f) * (float)Hf;
+        const float rw_ = fmaxf(fx2 - fx1, 1.f), rh_ = fmaxf(fy2 - fy1, 1.f);
+        x0 = min(x0, max((int)floorf(fx1) - 1, 0));
+        y0 = min(y0, max((int)floorf(fy1) - 1, 0));
+        x1 = max(x1, min((int)floorf(fx1 + rw_) + 2, Wf - 1));
+        y1 = max(y1, min((int)floorf(fy1 + rh_) + 2, Hf - 1));
+      }
+    }
+    s_fp[u] = make_int2(x0 | (x1 << 16), y0 | (y1 << 16));
   }
   __syncthreads();
   // this lane's 16-byte piece of a tap0 K-row: chunks 0-1 hi(t1), 2-3 hi(t2),
@@ -954,6 +982,8 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
     // 4q+p, ds_bpermute) leave lane (g, c) with channels 4c .. 4c+3.  The
     // 64-byte pieces of the plain fragment layout took ~35 us more per launch.
     const int src4 = ((lane & 0x30) | ((lane & 3) << 2) | ((lane >> 2) & 3)) * 4;
+    const int2 fp = s_fp[e_n];
+    const int fx0 = fp.x & 0xFFFF, fx1 = fp.x >> 16, fy0 = fp.y & 0xFFFF, fy1 = fp.y >> 16;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -967,7 +997,9 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
         const int Y = (int)(((float)q + 0.5f) * inv_rw), X = q - Y * rw;
         const unsigned o =
             (unsigned)((((e_n * Hf + 4 * Y + e_ca) * Wf + 4 * X + e_cb) * BN + wn * 64 + r16 * 4) * 4);
-        const unsigned so = q < RG && (DBG != 4 || (i | e) == 0) ? o : OOB;
+        const int py = 4 * Y + e_ca, px = 4 * X + e_cb;
+        const bool keep = q < RG && py >= fy0 && py <= fy1 && px >= fx0 && px <= fx1;
+        const unsigned so = keep && (DBG != 4 || (i | e) == 0) ? o : OOB;
         // nt: the 403 MB of output streams past the L2 instead of evicting the
         // weights and the next rounds' input rows (p.out_nt, A/B switch)
         if (p.out_nt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rout, so, 0, 2);
@@ -1057,8 +1089,8 @@ template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN
 __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   constexpr int NTH = NW * 64;
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
-  static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB && TPS == 1), "tenth tap: KH downsample");
-  static_assert(EMODE != 2 || (SPLIT && !DB && TPS == 1), "KH epilogue: split, one tap per K-step");
+  static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB), "tenth tap: KH downsample");
+  static_assert(EMODE != 2 || (SPLIT && !DB), "KH epilogue: split, single fragment set");
   constexpr int WAVES_N = BN / 64, WAVES_M = NW / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
   static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
@@ -1067,7 +1099,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   constexpr int B_LD = BN / 8 / NW;                      // B DMA wave-instructions per wave per K-step
   constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
   constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
-  static_assert(TPS == 1 || (SPLIT && 9 % TPS == 0), "taps per step");
+  static_assert(TPS == 1 || (SPLIT && NTAP % TPS == 0), "taps per step");
   constexpr bool FINAL = EMODE == 1;
   constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH, 128, NTH>();
   constexpr int LDS = RING > EPI ? RING : EPI;
@@ -1085,7 +1117,14 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   // channels as [hi32 | lo32] f16
   const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = NTAP * NC;
   stamp16(p.stamps, 0);
-  const i32x4 rin = make_rsrc(p.in, p.in_bytes), rwt = make_rsrc(p.wt, p.wt_bytes);
+  // the input descriptor starts at this tile's window (a 64-bit base), so
+  // the 31-bit buffer extent bounds the window, not the whole R-ROI tensor:
+  // one launch takes any number of ROIs (no per-chunk launches, each with
+  // its own partial last round of tiles)
+  const int wbase = max(m0 - 64, 0);
+  const i32x4 rin = make_rsrc(static_cast<const char*>(p.in) + (size_t)wbase * RB,
+                              (int)min(((long)Mtot - wbase) * RB, 0x7fffffffL));
+  const i32x4 rwt = make_rsrc(p.wt, p.wt_bytes);
   const unsigned lds0 = (unsigned)reinterpret_cast<unsigned long long>((lds_void*)lds);
   const int lrow = lane >> 3, lchunk = (lane & 7) ^ lrow;
   // A window: wave w fills rows [48 w, 48 w + 48) of the window
@@ -1093,7 +1132,7 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
     const int m = m0 - 64 + wave * (AWIN / NW) + i * 8 + lrow;
-    a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)(m * RB + lchunk * 16) : OOB;
+    a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)((m - wbase) * RB + lchunk * 16) : OOB;
   }
   unsigned b_off[B_LD];
 #pragma unroll
@@ -1709,7 +1748,10 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
   a.wt_bytes = (int)wt_bytes;
   a.m_off = 0;
   a.stagger = 0;
-  const int chunk = (int)std::min<long>(a0.R, kMaxDesc / roi_bytes);
+  // one launch for all ROIs (the kernel's input descriptor is per tile); the
+  // GEMM row index stays a 32-bit int
+  if ((long)a0.R * HPP >= 0x7fffffffL) return hipErrorInvalidValue;
+  const int chunk = a0.R;
   for (int r0 = 0; r0 < a0.R; r0 += chunk) {
     const int nr = std::min(chunk, a0.R - r0);
     a.R = nr;
@@ -1717,12 +1759,23 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
     a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
     if (a0.out) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.ns * 4;
     if (a0.outf) a.outf = a0.outf + (size_t)r0 * (HP - 2) * (HP - 2) * a.nf;
-    a.in_bytes = (int)(nr * roi_bytes);
+    a.in_bytes = (int)std::min<long>((long)nr * roi_bytes, kMaxDesc);   // (unused: per-tile descriptors)
     const long rows = (long)nr * HPP - 2 * HP;
     const dim3 grid((unsigned)((rows + BM - 1) / BM));
-    if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 3, 0, BM, true, 128, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
-    else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 32, 1, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
+    // two taps per K-step (three for the 32-channel conv): one barrier per
+    // 2-3 taps of MFMAs -- these convs have 96 / 32 / 16 live output columns,
+    // so a single tap's MFMAs are too few to amortise a barrier and the DMA
+    // issue (MFMA busy 0.37 at one tap per step).  KPD_KH_TPS1=1: one tap (A/B).
+    static const bool tps1 = kpd_diag_env("KPD_KH_TPS1") != nullptr;
+    if (tps1) {
+      if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 3, 0, BM, true, 128, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 32, 1, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
+    } else {
+      if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 2, 0, BM, true, 128, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 32, 3, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1743,14 +1796,17 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
   const long wt_bytes = (long)a.cout * 9 * a.cin * es, roi_bytes = (long)HPP * a.cin * es;
   if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
   a.wt_bytes = (int)wt_bytes;
-  const int chunk = (int)std::min<long>(a0.R, kMaxDesc / roi_bytes);
+  // one launch for all ROIs (the kernel's input descriptor is per tile, so
+  // the 31-bit extent bounds a tile's window only); row indices stay 32-bit
+  if ((long)a0.R * HPP >= 0x7fffffffL) return hipErrorInvalidValue;
+  const int chunk = a0.R;
   for (int r0 = 0; r0 < a0.R; r0 += chunk) {
     const int nr = std::min(chunk, a0.R - r0);
     a.R = nr;
     a.r0 = a0.r0 + r0;
     a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
     if (!fin) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.cout * es;
-    a.in_bytes = (int)(nr * roi_bytes);
+    a.in_bytes = (int)std::min<long>((long)nr * roi_bytes, kMaxDesc);   // (unused: per-tile descriptors)
     const long rows = (long)nr * HPP - 2 * HP;
     // BN 256 with a 2-stage weight ring measured faster than BN 128 with 4
     // stages for conv 1 / 2 (89 / 233 us vs 92 / 256 us at 64 ROIs): the

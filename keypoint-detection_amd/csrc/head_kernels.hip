@@ -13,6 +13,8 @@
 //
 // All ROIs of a batch are processed together as one [R,56,56,C] NHWC tensor
 // (R = B*P); the reference's per-box Python loop becomes grid dimensions.
+#include <algorithm>
+
 #include "kpd_common.h"
 #include "kpd_kernels.h"
 
@@ -157,22 +159,23 @@ __global__ void slotmap_kernel(const float* __restrict__ boxes, int B, int P, in
 // CW = channels per lane: 1 -> the 64 top-k channels (HeatmapHead input),
 // 2 -> all 128 FPN channels in order (KEYPOINT_HEAD input, topk == nullptr).
 constexpr int kRoiStageFloats = 12800;   // 50 KB (one interpolated row: 200 columns x 64 / 100 x 128 channels): 3 workgroups per CU
+// One output row ph of ROI r (all 56 bins) for CW x 64 channels: torchvision
+// roi_align sampling (aligned=False, sampling_ratio=-1) summed per bin in
+// acc[j][q] (bin pw = wave + 4 j, channel lane + 64 q, or topk[b][lane]);
+// divide by *count for the average.  stage: the dynamic LDS of stage_cap
+// floats for the separable path (stage_cap 0: direct gathers).
 template <int CW>
-__global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
-                                                        const int32_t* __restrict__ topk,
-                                                        const float* __restrict__ boxes, int P,
-                                                        float* __restrict__ roi, float* __restrict__ roi_stats,
-                                                        int stage_cap, unsigned long long* __restrict__ stamps) {
-  __shared__ float red[4][2][TOPK];
-  // diagnostic phase stamps (KPD_STAMPS): thread 0, s_memrealtime, row [8] per workgroup
+__device__ __forceinline__ void roi_row_sample(const float* __restrict__ feat, int Hf, int Wf, int Cf,
+                                               const int32_t* __restrict__ topk, const float* __restrict__ boxes,
+                                               int ph, int r, int b, int stage_cap, float* stage,
+                                               float (&acc)[HM / 4][CW], float* count_out,
+                                               unsigned long long* __restrict__ stamps) {
   auto stamp = [&](int i) {
     if (stamps && threadIdx.x == 0)
       stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
-  stamp(0);
-  constexpr int CO = TOPK * CW;
-  const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int CO = TOPK * CW;
   const float* bx = boxes + (size_t)r * 4;
   const float cx = bx[0], cy = bx[1], bw = bx[2], bh = bx[3];
   const float x1 = fminf(fmaxf(cx - bw / 2.f, 0.f), 1.f) * (float)Wf;
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   const float bin_w = roi_w / (float)HM, bin_h = roi_h / (float)HM;
   const int gw = (int)ceilf(roi_w / (float)HM), gh = (int)ceilf(roi_h / (float)HM);
   const float count = (float)max(gw * gh, 1);
+  *count_out = count;
   const float* fb = feat + (size_t)b * Hf * Wf * Cf;
 
   // The wave's 14 bins (pw = wave + 4 j) advance together through the
@@ -192,7 +196,6 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
   // arithmetic is the scalar loop's.  A sample outside [-1, H] x [-1, W]
   // contributes 0 (torchvision's skip).
   constexpr int NB = HM / 4;
-  float acc[NB][CW];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
 #pragma unroll
@@ -237,7 +240,6 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     staged = nc > 0 && nc * CO <= stage_cap;   // stage_cap: the launch's dynamic LDS (floats)
   }
   if (staged) {
-    extern __shared__ float stage[];
     int chs[CW];
 #pragma unroll
     for (int q = 0; q < CW; ++q) chs[q] = topk ? topk[b * TOPK + lane] : lane + TOPK * q;
@@ -301,37 +303,64 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     int yl = (int)yy, yh;
     if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
     const float ly = yy - (float)yl, hy = 1.f - ly;
-    for (int ix = 0; ix < gw; ++ix) {
-      float v[NB][4][CW], wgt[NB][4];
+    // the bins in groups of NBG (CW 2: two groups of 7 -- 14 bins x 4 corners
+    // x 2 channels of gathers in flight cost ~110 VGPRs and halved the
+    // resident waves); each bin still sums its samples in (iy, ix) order
+    constexpr int NBG = CW == 2 ? NB / 2 : NB;
+    for (int ix = 0; ix < gw; ++ix)
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int pw = wave + 4 * j;
+    for (int j0 = 0; j0 < NB; j0 += NBG) {
+      float v[NBG][4][CW], wgt[NBG][4];
+#pragma unroll
+      for (int jj = 0; jj < NBG; ++jj) {
+        const int j = j0 + jj, pw = wave + 4 * j;
         float x = x1 + (float)pw * bin_w + ((float)ix + 0.5f) * bin_w / (float)gw;
         const bool in = yin && !(x < -1.f || x > (float)Wf);
         float xx = x <= 0.f ? 0.f : x;
         int xl = (int)xx, xh;
         if (xl >= Wf - 1) { xh = xl = Wf - 1; xx = (float)xl; } else xh = xl + 1;
         const float lx = xx - (float)xl, hx = 1.f - lx;
-        wgt[j][0] = in ? hy * hx : 0.f; wgt[j][1] = in ? hy * lx : 0.f;
-        wgt[j][2] = in ? ly * hx : 0.f; wgt[j][3] = in ? ly * lx : 0.f;
+        wgt[jj][0] = in ? hy * hx : 0.f; wgt[jj][1] = in ? hy * lx : 0.f;
+        wgt[jj][2] = in ? ly * hx : 0.f; wgt[jj][3] = in ? ly * lx : 0.f;
         const float* p1 = fb + ((size_t)yl * Wf + xl) * Cf;
         const float* p2 = fb + ((size_t)yl * Wf + xh) * Cf;
         const float* p3 = fb + ((size_t)yh * Wf + xl) * Cf;
         const float* p4 = fb + ((size_t)yh * Wf + xh) * Cf;
 #pragma unroll
         for (int q = 0; q < CW; ++q) {
-          v[j][0][q] = p1[ch[q]]; v[j][1][q] = p2[ch[q]]; v[j][2][q] = p3[ch[q]]; v[j][3][q] = p4[ch[q]];
+          v[jj][0][q] = p1[ch[q]]; v[jj][1][q] = p2[ch[q]]; v[jj][2][q] = p3[ch[q]]; v[jj][3][q] = p4[ch[q]];
         }
       }
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
+      for (int jj = 0; jj < NBG; ++jj)
 #pragma unroll
         for (int q = 0; q < CW; ++q)
-          acc[j][q] += wgt[j][0] * v[j][0][q] + wgt[j][1] * v[j][1][q] + wgt[j][2] * v[j][2][q] +
-                       wgt[j][3] * v[j][3][q];
+          acc[j0 + jj][q] += wgt[jj][0] * v[jj][0][q] + wgt[jj][1] * v[jj][1][q] + wgt[jj][2] * v[jj][2][q] +
+                             wgt[jj][3] * v[jj][3][q];
     }
   }
   }
+}
+
+template <int CW>
+__global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict__ feat, int Hf, int Wf, int Cf,
+                                                        const int32_t* __restrict__ topk,
+                                                        const float* __restrict__ boxes, int P,
+                                                        float* __restrict__ roi, float* __restrict__ roi_stats,
+                                                        int stage_cap, unsigned long long* __restrict__ stamps) {
+  __shared__ float red[4][2][TOPK];
+  extern __shared__ float stage[];
+  constexpr int CO = TOPK * CW, NB = HM / 4;
+  const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (stamps && threadIdx.x == 0)
+    stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8] = __builtin_amdgcn_s_memrealtime();
+  float acc[NB][CW], count;
+  roi_row_sample<CW>(feat, Hf, Wf, Cf, topk, boxes, ph, r, b, stage_cap, stage, acc, &count, stamps);
+  auto stamp = [&](int i) {
+    if (stamps && threadIdx.x == 0)
+      stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
   stamp(2);
   float s_sum = 0.f, s_max = -INFINITY;
 #pragma unroll
@@ -357,6 +386,161 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
     st[TOPK + lane] = m;
   }
   stamp(3);
+}
+
+// ---------------------------------------------------------------- ROI align + KEYPOINT_HEAD attention
+// Dual-head forward, split precision: the two ROI aligns of a box (the 64
+// top-k channels for HeatmapHead, all 128 FPN channels for KEYPOINT_HEAD,
+// keypoint_model.py:212-228 / keypoint_head.py:51-54) sample the same
+// positions, so one pass over the 128 channels serves both, and
+// KEYPOINT_HEAD's spatial attention (keypoint_head.py:15-20,53-54:
+// att = sigmoid(b2 + w2 . relu6(W1 x + b1)), x * att) is per pixel, so it runs
+// on the row while it is in registers.  grid (56 rows, R), 256 threads; lane
+// = channels lane, lane + 64 (roi_row_sample<2>).  Outputs:
+//   roi / roi_stats: the top-k channels (lane <- channel topk[b][lane] by a
+//     cross-lane read), as roi_align_kernel<1> writes them;
+//   out: x * att * 2^a as the split [hi32 | lo32] operand of the first
+//     KEYPOINT_HEAD conv, interior of the zero-bordered [R][58][58][128] map
+//     (a = split_exp_of(bound of the image), hsc[r][2] = that bound), staged
+//     in LDS and stored as whole 28 KB rows;
+// replacing roi_align_kernel<1>, roi_align_kernel<2> (whose 128-channel fp32
+// map went through HBM twice) and kh_att2_kernel.  The attention's 1x1 128 ->
+// 64 runs on v_mfma_f32_16x16x32_f16 with the three split products (lo.hi,
+// hi.hi, hi.lo) and the 64 -> 1 dot by 16-lane butterflies and a 4-wave sum:
+// the arithmetic of kh_att2_kernel.
+constexpr int kKaRow = 528;   // LDS bytes per pixel of the attention operand: hi 256 | lo 256 | 16 pad
+constexpr int kRoiKhLds = 64 * kKaRow;   // (>= 56 x 512 output staging)
+__global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict__ feat, int Hf, int Wf,
+                                                     const int32_t* __restrict__ topk,
+                                                     const float* __restrict__ boxes, int P,
+                                                     float* __restrict__ roi, float* __restrict__ roi_stats,
+                                                     int stage_cap, const _Float16* __restrict__ w1s, int w1_exp,
+                                                     const float* __restrict__ b1, const float* __restrict__ w2,
+                                                     const float* __restrict__ b2, const float* __restrict__ bound,
+                                                     int bdiv, int bstride, float* __restrict__ hsc,
+                                                     _Float16* __restrict__ out) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  __shared__ float red[4][2][TOPK];
+  __shared__ float spart[4][64];
+  __shared__ float satt[64];
+  extern __shared__ __attribute__((aligned(16))) float stage[];
+  constexpr int NB = HM / 4;
+  const int ph = blockIdx.x, r = blockIdx.y, b = r / P;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int co = wave * 16 + r16;
+  const int tch = topk[b * TOPK + lane];
+  const float bnd = bound[(size_t)(r / bdiv) * bstride];
+  if (tid == 0 && ph == 0) hsc[(size_t)r * 4 + 2] = bnd;
+
+  float acc[NB][2], count;
+  roi_row_sample<2>(feat, Hf, Wf, 2 * TOPK, nullptr, boxes, ph, r, b, stage_cap, stage, acc, &count, nullptr);
+  // attention weights (wave w: output channels 16 w .. 16 w + 15), loaded
+  // after the sampling (held through it they cost the kernel its occupancy);
+  // their latency overlaps the top-k / statistics phase below
+  h8 bh[4], bl[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const _Float16* wp = w1s + (size_t)co * 256 + c * 64 + g * 8;
+    bh[c] = *reinterpret_cast<const h8*>(wp);
+    bl[c] = *reinterpret_cast<const h8*>(wp + 32);
+  }
+  const float bias1 = b1[co], wo2 = w2[co], bias2 = b2[0];
+  const int ea = split_exp_of(bnd);
+  const float sc = ldexpf(1.f, ea), us = ldexpf(1.f, -(ea + w1_exp));
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    acc[j][0] /= count;
+    acc[j][1] /= count;
+  }
+  // HeatmapHead input: channel topk[lane] of the row (held by lane tch & 63,
+  // slot tch >> 6 of the same wave) + the per-row channel sum / max partials
+  {
+    const int src = (tch & 63) * 4;
+    const bool hi_half = tch >= 64;
+    float s_sum = 0.f, s_max = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const float a0 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(acc[j][0])));
+      const float a1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(acc[j][1])));
+      const float v = hi_half ? a1 : a0;
+      roi[(((size_t)r * HM + ph) * HM + wave + 4 * j) * TOPK + lane] = v;
+      s_sum += v;
+      s_max = fmaxf(s_max, v);
+    }
+    red[wave][0][lane] = s_sum;
+    red[wave][1][lane] = s_max;
+  }
+  __syncthreads();   // every wave's reads of the sampling stage are done: it becomes the operand image
+  if (wave == 0) {
+    const float s = red[0][0][lane] + red[1][0][lane] + red[2][0][lane] + red[3][0][lane];
+    const float m = fmaxf(fmaxf(red[0][1][lane], red[1][1][lane]), fmaxf(red[2][1][lane], red[3][1][lane]));
+    float* st = roi_stats + ((size_t)r * HM + ph) * 2 * TOPK;
+    st[lane] = s;
+    st[TOPK + lane] = m;
+  }
+  char* img = reinterpret_cast<char*>(stage);
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float xs = acc[j][q] * sc;
+      const _Float16 hi = (_Float16)xs, lo = (_Float16)(xs - (float)hi);
+      char* rowp = img + (wave + 4 * j) * kKaRow + (lane + TOPK * q) * 2;
+      *reinterpret_cast<_Float16*>(rowp) = hi;
+      *reinterpret_cast<_Float16*>(rowp + 256) = lo;
+    }
+  __syncthreads();
+  // 1x1 128 -> 64 on 64 pixel rows (rows 56-63 are don't-care: every MFMA row
+  // depends on its own A row only, and their results are dropped)
+  f32x4 am[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) am[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const char* rowp = img + (i * 16 + r16) * kKaRow + c * 64 + g * 16;
+      const h8 ah = *reinterpret_cast<const h8*>(rowp), al = *reinterpret_cast<const h8*>(rowp + 256);
+      am[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[c], am[i], 0, 0, 0);
+      am[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[c], am[i], 0, 0, 0);
+      am[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[c], am[i], 0, 0, 0);
+    }
+  // lane (g, r16) holds pixels 16 i + 4 g + e of output channel co
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pv = wo2 * fminf(fmaxf(fmaf(am[i][e], us, bias1), 0.f), 6.f);
+      pv += __shfl_xor(pv, 1);
+      pv += __shfl_xor(pv, 2);
+      pv += __shfl_xor(pv, 4);
+      pv += __shfl_xor(pv, 8);
+      if (r16 == 0) spart[wave][i * 16 + g * 4 + e] = pv;
+    }
+  __syncthreads();   // (also: every wave's operand reads are done -- the image becomes the output stage)
+  if (tid < 64) satt[tid] = kpd_sigmoid(bias2 + ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid])));
+  __syncthreads();
+  // x * att * 2^a as f16 hi / lo in the [hi32 | lo32] groups of the padded map's row
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int pw = wave + 4 * j;
+    const float att = satt[pw];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = lane + TOPK * q;
+      const float xs = (acc[j][q] * att) * sc;
+      const _Float16 hi = (_Float16)xs, lo = (_Float16)(xs - (float)hi);
+      char* o = img + pw * 512 + (c >> 5) * 128 + (c & 31) * 2;
+      *reinterpret_cast<_Float16*>(o) = hi;
+      *reinterpret_cast<_Float16*>(o + 64) = lo;
+    }
+  }
+  __syncthreads();
+  // pixels 1..56 of padded row ph + 1 are one contiguous 28 KB run
+  uint4* dst = reinterpret_cast<uint4*>(out + (((size_t)r * (HM + 2) + ph + 1) * (HM + 2) + 1) * 256);
+  const uint4* srcs = reinterpret_cast<const uint4*>(img);
+#pragma unroll
+  for (int k = 0; k < HM * 512 / 16 / 256; ++k) dst[tid + 256 * k] = srcs[tid + 256 * k];
 }
 
 // ---------------------------------------------------------------- HeatmapHead channel attention
@@ -785,6 +969,22 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
     hipLaunchKernelGGL((roi_align_kernel<2>), dim3(HM, R), dim3(256), cap * 4, st, feat, Hf, Wf, Cf, nullptr, boxes, P,
                        roi, nullptr, cap, stamps);
   }
+  return hipGetLastError();
+}
+hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk, const float* boxes, int R, int P,
+                        float* roi, float* roi_stats, const void* w1s, int w1_exp, const float* b1, const float* w2,
+                        const float* b2, const float* bound, int bdiv, int bstride, float* hsc, void* out,
+                        hipStream_t st) {
+  if (R <= 0) return hipSuccess;
+  if (!topk || !roi || !roi_stats || !w1s || !bound || bdiv < 1 || bstride < 1 || !hsc || !out)
+    return hipErrorInvalidValue;
+  // the sampling stage sized to the map width (128 channels), at least the
+  // attention operand image it becomes afterwards
+  const int cap = std::min(kRoiStageFloats, Wf * 2 * TOPK);
+  const size_t lds = std::max<size_t>((size_t)cap * 4, kRoiKhLds);
+  hipLaunchKernelGGL(roi_kh_kernel, dim3(HM, R), dim3(256), lds, st, feat, Hf, Wf, topk, boxes, P, roi, roi_stats,
+                     cap, static_cast<const _Float16*>(w1s), w1_exp, b1, w2, b2, bound, bdiv, bstride, hsc,
+                     static_cast<_Float16*>(out));
   return hipGetLastError();
 }
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,

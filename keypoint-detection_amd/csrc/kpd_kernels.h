@@ -121,6 +121,12 @@ struct Fpn0xArgs {
   int stagger;             // launcher: waves 4-7 issue their K-loop DMA one pass later
   int out_nt;              // launcher: non-temporal output stores
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
+  // footprint stores (boxes != null): image n's output pixels are stored only
+  // inside the rectangle its ROI aligns read -- the union over its fp_P
+  // cxcywh boxes [fp_NB][fp_P][4] of the sampled rows / columns, one pixel of
+  // margin; images >= fp_NB store nothing
+  const float* fp_boxes;
+  int fp_NB, fp_P;
 };
 hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st);
 // fp32 NHWC -> f16 hi|lo split rows (groups of 32 channels, or 16 for cin 16),
@@ -249,6 +255,13 @@ hipError_t launch_topk(const float* stats, int N, int tiles, int HW, const float
                        float* sc_zero = nullptr, int sc_n = 0);
 hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
+// Dual head, split precision: one 128-channel ROI align pass writing the top-k
+// HeatmapHead input (roi, roi_stats) and KEYPOINT_HEAD's attention-applied
+// split operand (out: [R][58][58][128] hi|lo f16 interior; hsc[r][2] = bound)
+hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk, const float* boxes, int R, int P,
+                        float* roi, float* roi_stats, const void* w1s, int w1_exp, const float* b1, const float* w2,
+                        const float* b2, const float* bound, int bdiv, int bstride, float* hsc, void* out,
+                        hipStream_t st);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
                             const float* boxes, int R, int P, float* roi, float* roi_stats,
                             hipStream_t st, unsigned long long* stamps = nullptr);   // stamps: KPD_STAMPS [grid][8]

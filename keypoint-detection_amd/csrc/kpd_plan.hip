@@ -1244,8 +1244,10 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
 // KEYPOINT_HEAD (keypoint_head.py:50-62, ResidualBlock :64-90) on the
 // [R][56][56][128] NHWC ROI features in w.kx; outputs at the ROIs' slots.
 // bound (split path): the bound of |x| for ROI r is bound[(r / bdiv) * bstride]
+// x_ready: the first conv's split operand (x * attention) is already in
+// w.kxs (roi_kh_kernel wrote it with the HeatmapHead's ROI align).
 static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st,
-                             const float* bound, int bdiv, int bstride) {
+                             const float* bound, int bdiv, int bstride, bool x_ready = false) {
   const size_t px = (size_t)R * 3136;
   if (p->kh_split && w.kxs) {
     // fp32-accurate split products on zero-bordered maps (hmconv_kernel MODE 2):
@@ -1255,7 +1257,9 @@ static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts,
     // attention (1x1 convs + sigmoid + apply) is one kernel writing the first
     // conv's operand (KPD_KH_ATT1=1: the fp32 1x1 conv + apply kernel, A/B).
     static const bool att1 = kpd_diag_env("KPD_KH_ATT1") != nullptr;
-    if (att1 || !p->kh_sa1.ws) {
+    if (x_ready) {
+      // (roi_kh_kernel)
+    } else if (att1 || !p->kh_sa1.ws) {
       if (int rc = conv(p->kh_sa1, w.kx, R, 56, 56, 128, w.ksa, ACT_RELU6, nullptr, 0, 0, nullptr, nullptr, 0, 0, st))
         return rc;
       HIP_TRY(launch_kh_att_split(w.kx, w.ksa, p->kh_sa2_w, p->kh_sa2_b, R, bound, bdiv, bstride, w.hsc, w.kxs, st));
@@ -1348,7 +1352,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     return KPD_OK;
   };
   Dims d;
-  d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P; d.flags = flags;
+  d.B = B; d.H = H; d.W = W; d.NB = NB; d.P = P; d.flags = flags & ~KPD_FLAG_FULL_LEVEL0;   // (no workspace effect)
   d.h[0] = (H - 1) / 2 + 1; d.w[0] = (W - 1) / 2 + 1;
   for (int i = 0; i < 11; ++i) {
     const int k = kBneck[i].k, s = kBneck[i].s, pd = (k - 1) / 2;
@@ -1587,6 +1591,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   lat_stage.reset();
   if (int rc = mark(2)) return rc;
   std::unique_ptr<Stage> fpn_stage(new Stage(p, "fpn0", st));
+  // caller boxes: level 0 is stored only where the ROI aligns read it (the
+  // 400 MB fp32 map per 64 images otherwise; KPD_FLAG_FULL_LEVEL0 stores all)
+  const bool footprint = lin && !detect && boxes && NB * P > 0 && !(flags & KPD_FLAG_FULL_LEVEL0) && p->has_ca;
   if (lin) {
     Fpn0xArgs a{};
     char* base = reinterpret_cast<char*>(w.lat[0]);
@@ -1605,6 +1612,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     a.l_bytes = (int)std::min<size_t>((size_t)B * lh[1] * lw[1] * 512, 0x7fffffff);
     a.w0_bytes = p->fpn0x.w0_bytes; a.weff_bytes = p->fpn0x.weff_bytes;
     a.stamps = take_stamps("stamps_fpn0x", (size_t)16 * B * tpc);
+    if (footprint) {
+      a.fp_boxes = boxes; a.fp_NB = NB; a.fp_P = P;
+    }
     HIP_TRY(launch_fpn0x(a, st));
   } else if (int rc = conv(p->fpn0, w.lat[0], B, d.Hf, d.Wf, 128, w.feat, ACT_RELU, nullptr, 0, 0, nullptr,
                            d.fused_stats ? w.stats : nullptr, d.tiles, 0, st)) {
@@ -1624,7 +1634,7 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   topk_stage.reset();
   if (int rc = mark(4)) return rc;
   if (topk_out) HIP_TRY(hipMemcpyAsync(topk_out, w.topk, sizeof(int32_t) * B * 64, hipMemcpyDeviceToDevice, st));
-  dbg["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
+  if (!footprint) dbg["feat0"] = {w.feat, sizeof(float) * (size_t)B * HWf * 128};
   dbg["scores"] = {w.scores, sizeof(float) * (size_t)B * 128};
   dbg["tap0"] = {taps[0], sizeof(float) * (size_t)B * lh[0] * lw[0] * 16};
   dbg["tap1"] = {taps[1], sizeof(float) * (size_t)B * lh[1] * lw[1] * pad16(24)};
@@ -1652,11 +1662,21 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   float* heat_out = heat ? heat : w.heat;
   // no output memsets: the padding slots are written (zeros / dummy person) by
   // hm_final_kernel, decode_kernel and kh_final_kernel through the slot map
+  // dual head, split: one ROI-align pass for both heads with KEYPOINT_HEAD's
+  // spatial attention fused (roi_kh_kernel); KPD_NO_ROI_KH=1: the separate
+  // launches (A/B)
+  static const bool no_roi_kh = kpd_diag_env("KPD_NO_ROI_KH") != nullptr;
+  const bool roi_kh = dual && p->kh_split && w.kxs && p->kh_sa1.ws && !no_roi_kh &&
+                      kpd_diag_env("KPD_KH_ATT1") == nullptr;
   {
     Stage sg(p, "roi_align", st);
     if (!slot_in_topk) HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
-    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st,
-                             take_stamps("stamps_roi_0", (size_t)56 * R)));
+    if (roi_kh)
+      HIP_TRY(launch_roi_kh(w.feat, d.Hf, d.Wf, w.topk, boxes, R, P, w.roi, w.roi_stats, p->kh_sa1.ws,
+                            p->kh_sa1.w_exp, p->kh_sa1.b, p->kh_sa2_w, p->kh_sa2_b, w.imax, P, 1, w.hsc, w.kxs, st));
+    else
+      HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st,
+                               take_stamps("stamps_roi_0", (size_t)56 * R)));
   }
   if (int rc = mark(5)) return rc;
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
@@ -1672,8 +1692,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   if (dual) {
     // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
     Stage sg(p, "keypoint_head", st);
-    HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
-    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1)) return rc;
+    if (!roi_kh) HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
+    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1, roi_kh)) return rc;
   }
   return KPD_OK;
 }
@@ -1800,7 +1820,7 @@ static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, in
     return fail(KPD_ESTATE, "plan lacks backbone / fpn / channel_attention / heatmap_head weights");
   if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
   if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
-  if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD)) return fail(KPD_EINVAL, "unknown flags");
+  if (flags & ~(KPD_FLAG_DETECT | KPD_FLAG_DUAL_HEAD | KPD_FLAG_FULL_LEVEL0)) return fail(KPD_EINVAL, "unknown flags");
   const bool detect = flags & KPD_FLAG_DETECT, dual = flags & KPD_FLAG_DUAL_HEAD;
   if (detect && (NB != B || P <= 0 || !boxes)) return fail(KPD_EINVAL, "detect mode: boxes must be [B][P>0][4]");
   if (detect && !p->anchors) return fail(KPD_ESTATE, "person detector weights missing");

@@ -35,6 +35,7 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_conv3x3_backward", "kpd_plan_set_graphs")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
+FLAG_FULL_LEVEL0 = 4   # store all of FPN level 0 (debug copy "feat0"); default: only the ROI-align footprints
 HEAD_CHANNEL_ATT, HEAD_SPATIAL_ATT, HEAD_CONVS, HEAD_ALL = 1, 2, 4, 7
 DECODE_ARGMAX, DECODE_SUBPIXEL, DECODE_SOFTARGMAX, DECODE_MODEL = 0, 1, 2, 3
 STAGES = ("body", "fpn_lateral", "fpn0", "topk", "person_detect", "roi_align", "hm_attention", "hm_conv1",

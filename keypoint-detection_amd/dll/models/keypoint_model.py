@@ -117,6 +117,11 @@ class MultiPersonKeypointModel(nn.Module):
                  accumulation (keypoints within 1e-3); the backbone/FPN feeding
                  the order-critical channel top-k stays fp32-accurate.
       dual_head: also instantiate KEYPOINT_HEAD (not wired in the reference).
+
+    Attribute ``full_level0`` (default False): with caller boxes the native
+    path stores FPN level 0 only where the ROI aligns read it; True stores
+    the whole map (for inspecting ``native_plan(dev).debug_buffer("feat0")``).
+    Outputs are identical either way.
     """
 
     def __init__(self, config: ModelConfig, training_config: TrainingConfig, precision: str = "split",
@@ -137,6 +142,7 @@ class MultiPersonKeypointModel(nn.Module):
         self.num_keypoints = config.num_keypoints
         self.precision = precision      # (property: also sets the submodules' own plans' precision)
         self.streams = streams          # sub-batch streams for B >= 32 (kpd_plan_set_streams)
+        self.full_level0 = False        # store all of FPN level 0 (debug copy), not just the ROI footprints
         self._plan: Optional[_native.Plan] = None
         self._plan_key = None
         self._plan_streams: Optional[int] = None
@@ -218,7 +224,8 @@ class MultiPersonKeypointModel(nn.Module):
         boxes = normalize_bboxes(batch, B, dev)
         plan = self.native_plan(dev)
         image = x.float().contiguous()
-        flags = _native.FLAG_DUAL_HEAD if self.dual_head else 0
+        flags = (_native.FLAG_DUAL_HEAD if self.dual_head else 0) | \
+            (_native.FLAG_FULL_LEVEL0 if self.full_level0 else 0)
         if boxes is None:
             # person-detector branch (reference :114-119 is broken; build-defined
             # glue: FPN0 -> 56x56 pool -> box/cls heads -> decode -> NMS,

@@ -23,12 +23,13 @@ def _np(p):
     return np.load(p, allow_pickle=False)
 
 
-def _model(sd, precision="fp32", in_channels=3):
+def _model(sd, precision="fp32", in_channels=3, full_level0=False):
     from dll.configs import BackboneConfig, ModelConfig, TrainingConfig
     from dll.models import MultiPersonKeypointModel
     m = MultiPersonKeypointModel(ModelConfig(backbone=BackboneConfig(in_channels=in_channels)), TrainingConfig(),
                                  precision=precision)
     m.load_state_dict(sd)
+    m.full_level0 = full_level0    # tests reading the "feat0" debug copy store the whole map
     return m.to(DEV).eval()
 
 
@@ -41,7 +42,7 @@ def _nchw_feat(plan, B, Hf, Wf):
 def test_forward_main_vs_golden(golden_dir, model_sd, precision):
     from dll.models.synthetic import synthetic_images
     g = _np(golden_dir / "forward_main.npz")
-    m = _model(model_sd, precision)
+    m = _model(model_sd, precision, full_level0=True)
     img = synthetic_images(2, 3, 256, 192, seed=1234, device=DEV)
     boxes = torch.from_numpy(g["boxes"]).to(DEV)
     with torch.no_grad():
@@ -72,6 +73,34 @@ def test_forward_main_vs_golden(golden_dir, model_sd, precision):
         np.testing.assert_allclose(hm[0, 0].numpy(), g["heatmap_b0p0"], atol=3e-2)
     # compacted + padded slot of the zero box (image 1, slot 2) is all zero
     assert not out["keypoints"][1, 2].any() and not out["visibilities"][1, 2].any()
+
+
+@pytest.mark.parametrize("precision", ["split", "mixed"])
+def test_level0_footprint_stores(model_sd, precision):
+    """With caller boxes FPN level 0 is stored only where the ROI aligns read
+    it (fpn0x_kernel footprint rectangles): every output equals the
+    full-map forward's bit for bit -- boxes at the borders, tiny and
+    full-image boxes, zero boxes mid-list, an image with no valid box and one
+    past the box list -- and the default forward has no "feat0" debug copy."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    img = synthetic_images(5, 3, 256, 192, seed=71, device=DEV)
+    boxes = synthetic_boxes(4, 3, seed=72, device=DEV)
+    boxes[0, 1] = torch.tensor([0.02, 0.98, 0.05, 0.03])      # corner, sub-pixel
+    boxes[1, 0] = torch.tensor([0.5, 0.5, 1.0, 1.0])          # whole image
+    boxes[1, 2] = 0.0                                          # zero box mid-list
+    boxes[2] = 0.0                                             # no valid box: dummy person
+    boxes[3, 2] = torch.tensor([0.99, 0.5, 0.4, 0.2])         # right border
+    outs = []
+    for full in (True, False):
+        m = _model(model_sd, precision, full_level0=full)
+        with torch.no_grad():
+            outs.append(m({"image": img, "bboxes": [boxes]}))
+        if not full:
+            with pytest.raises(ValueError):
+                m.native_plan(DEV).debug_buffer("feat0")
+    a, b = outs
+    for k in ("keypoints", "visibilities", "heatmap"):
+        assert torch.equal(a[k], b[k]), k
 
 
 def test_forward_dummy_empty(golden_dir, model_sd):
@@ -118,7 +147,7 @@ def test_odd_size_vs_oracle(model_sd, precision):
     boxes = torch.tensor([[[0.5, 0.5, 0.9, 0.95], [0.02, 0.03, 0.1, 0.1], [0.98, 0.97, 0.3, 0.4]],
                           [[0.3, 0.6, 0.001, 0.002], [0.5, 0.5, 1.0, 1.0], [0.7, 0.2, 0.4, 0.3]]])
     ref = O.forward(model_sd, {"image": img, "bboxes": boxes}, return_debug=True)
-    m = _model(model_sd, precision)
+    m = _model(model_sd, precision, full_level0=True)
     with torch.no_grad():
         out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
     plan = m.native_plan(DEV)
@@ -143,7 +172,7 @@ def test_large_map_lateral_fallback(model_sd, precision):
     img = synthetic_images(1, 3, 480, 384, seed=9)
     boxes = torch.tensor([[[0.45, 0.55, 0.4, 0.7]]])
     ref = O.forward(model_sd, {"image": img, "bboxes": boxes}, return_debug=True)
-    m = _model(model_sd, precision)
+    m = _model(model_sd, precision, full_level0=True)
     with torch.no_grad():
         out = m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
     plan = m.native_plan(DEV)
@@ -158,7 +187,7 @@ def test_roi_features_vs_oracle(model_sd):
     from dll.models.synthetic import synthetic_boxes, synthetic_images
     img = synthetic_images(2, 3, 256, 192, seed=21)
     boxes = synthetic_boxes(2, 2, seed=22)
-    m = _model(model_sd)
+    m = _model(model_sd, full_level0=True)
     with torch.no_grad():
         m({"image": img.to(DEV), "bboxes": boxes.to(DEV)})
     plan = m.native_plan(DEV)
@@ -285,7 +314,9 @@ def _check_detections(got_boxes, got_scores, ref_boxes, ref_scores, what):
 def test_person_detector_glue_vs_oracle(precision):
     """No 'bboxes' -> build-defined detector glue (§8 a10): pooled 1x1 heads,
     anchor decode, threshold, NMS (max 5).  At BASELINE C3's size (B = 256,
-    256x192, two sub-batch streams) in every precision, with a dynamic-range
+    256x192, one stream: the debug copy of FPN level 0 needs a single pass;
+    test_c4_rank_shard_bit_identical covers the detector at two streams) in
+    every precision, with a dynamic-range
     outlier in the batch.  Nine images are checked twice against the oracle:
     on the GPU's own FPN level 0 (isolates the glue) and on the oracle's FPN
     level 0 computed from the image (the whole detector path, so a split-mode
@@ -293,7 +324,6 @@ def test_person_detector_glue_vs_oracle(precision):
     the keypoint stage on the detected boxes."""
     from dll.models.synthetic import synthetic_images
     m, sd = _dual_model(precision)
-    m.streams = 2
     B = 256
     img = synthetic_images(B, 3, 256, 192, seed=51, device=DEV)
     img[17] *= 4.0                             # dynamic-range outlier (x25 saturates the

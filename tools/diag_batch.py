@@ -16,6 +16,7 @@ dev = torch.device("cuda:0")
 m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=prec)
 m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
 m = m.to(dev).eval()
+m.full_level0 = True   # the "feat0" debug copy below needs the whole map
 B = 6
 img = synthetic_images(B, 3, 256, 192, seed=31, device=dev)
 img[3] *= 40.0

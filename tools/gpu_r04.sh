@@ -91,6 +91,25 @@ for k, v in m.items():
                   if c in ("avg_us", "hbm_bytes_per_launch", "mfma_busy_frac")})
 PY
     ;;
+  ab)
+    # same-box A/B of diagnostic switches on the diagnostic build (make diag):
+    # AB_ENVS="NAME=1;NAME2=1" (";"-separated variants, "-" = none), AB_CFG c2|c3
+    IFS=";" read -ra VARS <<< "${AB_ENVS:--}"
+    for rep in 1 2; do
+      for V in "${VARS[@]}"; do
+        if [ "${AB_CFG:-c3}" = c3 ]; then ARGS="--c3-only --steps 10 --warmup 5 --no-cpu-baseline --alt-streams 0"
+        else ARGS="--steps 20 --warmup 10 --no-cpu-baseline --c3 0 --secondary split --alt-streams 0"; fi
+        if [ "$V" = "-" ]; then E=""; else E="$V"; fi
+        env KPD_DIAG_LIB=1 $E timeout -k 10 300 python3 bench.py $ARGS > "$OUT/ab.json" 2> "$OUT/ab.err" \
+          || { echo "ab rc=$? ($V)"; tail -5 "$OUT/ab.err"; exit 1; }
+        python3 - "$OUT/ab.json" "$V" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+c = d.get("configs", {}).get("C3") or d
+print(sys.argv[2], "value", c["value"], "ms", c["ms_per_step"], {k: round(v, 3) for k, v in c["stages_ms"].items()})
+PY
+      done
+    done ;;
   *) echo "unknown step $S"; exit 1 ;;
   esac
 done
