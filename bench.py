@@ -80,11 +80,13 @@ def flops_per_image(H, W, P, in_ch=3):
             "hm_conv3": hm_convs[2] * P}
 
 
-def kh_flops_per_roi(c=128, fine=64, reg=32, vis=32, h=56, w=56):
+def kh_flops_per_roi(c=128, fine=64, reg=32, vis=32, h=56, w=56, attention=True):
     """KEYPOINT_HEAD algorithmic flops per ROI (keypoint_head.py:9-90): 2*MAC
-    of its convs and linears at the ROI resolution (BN folded)."""
+    of its convs and linears at the ROI resolution (BN folded); attention=False
+    leaves out the spatial attention's 1x1 convs (fused into the ROI align
+    kernel, roi_kh_kernel, so timed in the roi_align stage)."""
     hw = h * w
-    f = 2.0 * hw * (c * (c // 2) + (c // 2))                        # spatial attention 1x1 C->C/2->1
+    f = 2.0 * hw * (c * (c // 2) + (c // 2)) if attention else 0.0   # spatial attention 1x1 C->C/2->1
     f += 2.0 * hw * (c * fine * 9 + (c * fine if c != fine else 0))  # ResidualBlock(C->64) (+ downsample)
     f += 2.0 * hw * (fine * reg * 9 + (fine * reg if fine != reg else 0))
     f += 2.0 * hw * reg * (reg // 2) * 9                               # 3x3 32->16
@@ -101,6 +103,7 @@ def config_flops(H, W, P, detect):
     fl = dict(flops_per_image(H, W, P))
     kh = kh_flops_per_roi()
     fl["keypoint_head"] = P * kh
+    fl["keypoint_head_convs"] = P * kh_flops_per_roi(attention=False)
     fl["total"] += P * kh + (2.0 * 3136 * 128 * 45 if detect else 0.0)
     return fl
 
@@ -482,7 +485,14 @@ def run_c3(a, dev, pmc, cpu=True):
            "roofline": roof, "stages_ms": {k: round(v, 4) for k, v in stages.items()},
            "stage_launches_per_forward": launches}
     if "keypoint_head" in stages:
-        res["keypoint_head_tflops"] = round(fl["keypoint_head"] * B / nl / (stages["keypoint_head"] * 1e-3) / 1e12, 2)
+        # the keypoint_head stage runs the KEYPOINT_HEAD convs, pools and linears; its spatial attention
+        # (1x1 128->64->1) is fused into the roi_align stage's kernel (roi_kh_kernel) in split precision
+        fused = a.precision != "fp32"
+        kf = fl["keypoint_head_convs"] if fused else fl["keypoint_head"]
+        res["keypoint_head_tflops"] = round(kf * B / nl / (stages["keypoint_head"] * 1e-3) / 1e12, 2)
+        res["keypoint_head_note"] = ("algorithmic KEYPOINT_HEAD flops of the keypoint_head stage / its time"
+                                     + ("; the spatial attention's 1x1 convs run fused in the roi_align stage"
+                                        if fused else ""))
     if a.alt_streams and a.alt_streams != 1:
         m.streams = a.alt_streams
         el2, out2 = run_steps(a.steps, a.warmup, step, False)
@@ -659,7 +669,9 @@ def main(argv=None):
         "roofline": roof,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "stages_note": f"per launch (one sub-batch of {Bl} images): one forward with every stage's HIP events "
-                       "before the timed region; the dominant stage's figure is its timed-region mean",
+                       "before the timed region; the dominant stage's figure is its timed-region mean.  Not a "
+                       "partition of ms_per_step: the event-instrumented forward leaves a gap at every stage "
+                       "boundary (so the stages sum to more than a step), and ms_per_step is a wall-clock mean",
         "cpu_baseline": None,
     }
     if world == 1 and a.alt_streams and a.alt_streams != a.streams and B // 16 >= 2:

@@ -959,6 +959,7 @@ constexpr int FIR_CS = 16;
 template <int K, int S>
 __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int PD = (K - 1) / 2, CS = FIR_CS, CQ = CS / 4;
   const int n = blockIdx.y, oy0 = blockIdx.x * a.TH, tid = threadIdx.x;
   const int TH = min(a.TH, a.Ho - oy0), Wi = a.Wi, Wo = a.Wo, cin_p = a.cin_p, cout_p = a.cout_p;
@@ -1003,11 +1004,11 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
   const bool has_unit = tid < units;
   const int u_pair = tid / nco8, u_co = (tid - u_pair * nco8) * 8;
   const int px0 = min(u_pair * 2, npx - 1), px1 = min(u_pair * 2 + 1, npx - 1);
-  float acc[2][8];
+  f2 acc[2][4];   // (channel pairs: packed FMAs)
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[r][j] = 0.f;
+    for (int j = 0; j < 4; ++j) acc[r][j] = f2{0.f, 0.f};
 
   // a slice's weights are loaded into registers one slice ahead (issued
   // before this slice's compute, stored to LDS after its barrier), so no
@@ -1060,10 +1061,13 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
     const int pg_n = (npx_in + 3) / 4;
     for (int i = tid; i < pg_n * CQ; i += 256) {
       const int pg = i / CQ, q = i - pg * CQ;
+      // (v_pk_fma_f32: channel pairs (x, y) / (z, w) in one packed FMA, the
+      // pixel value broadcast -- the same fma per element, half the VALU issue;
+      // the kernel is bound by its FMA issue)
       const float4 b = reinterpret_cast<const float4*>(sb)[q];
-      float acc_e[4][4];
+      f2 acc_e[4][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { acc_e[r][0] = b.x; acc_e[r][1] = b.y; acc_e[r][2] = b.z; acc_e[r][3] = b.w; }
+      for (int r = 0; r < 4; ++r) { acc_e[r][0] = f2{b.x, b.y}; acc_e[r][1] = f2{b.z, b.w}; }
       int pxr[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) pxr[r] = min(r * pg_n + pg, npx_in - 1);   // pixels pg_n apart: conflict-free xs reads
@@ -1078,8 +1082,8 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
           const float xk[4] = {xv[r].x, xv[r].y, xv[r].z, xv[r].w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            acc_e[r][0] = fmaf(xk[j], wv[j].x, acc_e[r][0]); acc_e[r][1] = fmaf(xk[j], wv[j].y, acc_e[r][1]);
-            acc_e[r][2] = fmaf(xk[j], wv[j].z, acc_e[r][2]); acc_e[r][3] = fmaf(xk[j], wv[j].w, acc_e[r][3]);
+            acc_e[r][0] = __builtin_elementwise_fma(f2{xk[j], xk[j]}, f2{wv[j].x, wv[j].y}, acc_e[r][0]);
+            acc_e[r][1] = __builtin_elementwise_fma(f2{xk[j], xk[j]}, f2{wv[j].z, wv[j].w}, acc_e[r][1]);
           }
         }
       }
@@ -1090,8 +1094,8 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
         const int iy = iy0 + px / Wi;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);   // the depthwise zero padding of the expanded tensor
         if (iy >= 0 && iy < a.Hi)
-          v = make_float4(kpd_act(acc_e[r][0], a.act_e), kpd_act(acc_e[r][1], a.act_e),
-                          kpd_act(acc_e[r][2], a.act_e), kpd_act(acc_e[r][3], a.act_e));
+          v = make_float4(kpd_act(acc_e[r][0].x, a.act_e), kpd_act(acc_e[r][0].y, a.act_e),
+                          kpd_act(acc_e[r][1].x, a.act_e), kpd_act(acc_e[r][1].y, a.act_e));
         reinterpret_cast<float4*>(es)[esw(px) * CQ + q] = v;
       }
     }
@@ -1102,9 +1106,9 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
     const int wx = (Wo + XT - 1) / XT;
     for (int i = tid; i < TH * wx * CQ; i += 256) {
       const int q = i % CQ, r = i / CQ, xt = r % wx, oy = r / wx, ox0 = xt * XT, ix0 = ox0 * S - PD;
-      float4 d[XT];
+      f2 d[XT][2];
 #pragma unroll
-      for (int o = 0; o < XT; ++o) d[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int o = 0; o < XT; ++o) d[o][0] = d[o][1] = f2{0.f, 0.f};
 #pragma unroll
       for (int ky = 0; ky < K; ++ky) {
         const int ly = oy * S + ky;   // row in the tile (iy = iy0 + ly)
@@ -1121,8 +1125,8 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
 #pragma unroll
           for (int o = 0; o < XT; ++o) {
             const float4 v = col[o * S + kx];
-            d[o].x = fmaf(v.x, w.x, d[o].x); d[o].y = fmaf(v.y, w.y, d[o].y);
-            d[o].z = fmaf(v.z, w.z, d[o].z); d[o].w = fmaf(v.w, w.w, d[o].w);
+            d[o][0] = __builtin_elementwise_fma(f2{v.x, v.y}, f2{w.x, w.y}, d[o][0]);
+            d[o][1] = __builtin_elementwise_fma(f2{v.z, v.w}, f2{w.z, w.w}, d[o][1]);
           }
         }
       }
@@ -1131,8 +1135,8 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
       for (int o = 0; o < XT; ++o) {
         if (ox0 + o >= Wo) break;
         float4 v;
-        v.x = kpd_act(d[o].x + b.x, a.act_d); v.y = kpd_act(d[o].y + b.y, a.act_d);
-        v.z = kpd_act(d[o].z + b.z, a.act_d); v.w = kpd_act(d[o].w + b.w, a.act_d);
+        v.x = kpd_act(d[o][0].x + b.x, a.act_d); v.y = kpd_act(d[o][0].y + b.y, a.act_d);
+        v.z = kpd_act(d[o][1].x + b.z, a.act_d); v.w = kpd_act(d[o][1].y + b.w, a.act_d);
         reinterpret_cast<float4*>(ds)[(oy * Wo + ox0 + o) * CQ + q] = v;
       }
     }
@@ -1149,11 +1153,11 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
         for (int cc = 0; cc < 4; ++cc) {
           const float4 w0 = *reinterpret_cast<const float4*>(wpT + (c4 * 4 + cc) * cout_p + u_co);
           const float4 w1 = *reinterpret_cast<const float4*>(wpT + (c4 * 4 + cc) * cout_p + u_co + 4);
-          const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+          const f2 wv[4] = {f2{w0.x, w0.y}, f2{w0.z, w0.w}, f2{w1.x, w1.y}, f2{w1.z, w1.w}};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            acc[0][j] = fmaf(dv0[cc], wv[j], acc[0][j]);
-            acc[1][j] = fmaf(dv1[cc], wv[j], acc[1][j]);
+          for (int j = 0; j < 4; ++j) {
+            acc[0][j] = __builtin_elementwise_fma(f2{dv0[cc], dv0[cc]}, wv[j], acc[0][j]);
+            acc[1][j] = __builtin_elementwise_fma(f2{dv1[cc], dv1[cc]}, wv[j], acc[1][j]);
           }
         }
       }
@@ -1170,7 +1174,7 @@ __global__ __launch_bounds__(256) void fir_kernel(const FirArgs a) {
     const int oy = oy0 + px / Wo, ox = px % Wo;
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = acc[r][j] + bv[j];
+    for (int j = 0; j < 8; ++j) v[j] = acc[r][j / 2][j % 2] + bv[j];
     if (a.res) {   // stride 1: the residual pixel is the output pixel
       const float* xr = xg + ((size_t)oy * Wi + ox) * cin_p + u_co;
       const float4 r0 = *reinterpret_cast<const float4*>(xr), r1 = *reinterpret_cast<const float4*>(xr + 4);

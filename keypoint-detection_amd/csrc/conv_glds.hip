@@ -604,7 +604,19 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   // latency overlaps this tile's epilogue.
   const int ntiles = 16 * p.N * p.tpc, G = gridDim.x;
   const int rb = xcd_remap(blockIdx.x, G);
-  auto tile_at = [&](int k) { return k * G + (rb + k) % G; };
+  // Class-half order (p.order == 1): rounds come in pairs over the same G / 8
+  // (image, row block) pairs, the first round of a pair taking position
+  // classes 0-7, the second 8-15.  An XCD then holds 4 row blocks x 8
+  // classes per round: half the per-class weights (the 2.3 MB of 16 classes
+  // re-fetched by every XCD every round dominated the kernel's HBM reads),
+  // while the row blocks' input rows stay in its L2 for the second half.
+  // The (rb + k) rotation still walks each workgroup through the classes.
+  const int NJ = p.N * p.tpc, NJR = G >> 3;
+  auto tile_at = [&](int k) {
+    if (!p.order) return k * G + (rb + k) % G;
+    const int r = (rb + k) % G, nj = (k >> 1) * NJR + (r >> 3);
+    return nj < NJ ? nj * 16 + (k & 1) * 8 + (r & 7) : ntiles;
+  };
 
   const i32x4 rf = make_rsrc(p.f_split, p.f_bytes), rl = make_rsrc(p.l_split, p.l_bytes);
   const i32x4 rw0 = make_rsrc(p.w0, p.w0_bytes), rwe = make_rsrc(p.weff, p.weff_bytes);
@@ -1144,7 +1156,12 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / NW) + i * 8) * ROWB);
     glds16(rin, dst, a_off[i] == OOB ? OOB : a_off[i] + c * 128, 0);
   };
+  // KH mode, 2-stage ring (every barrier waits vmcnt(0), so a wave's count of
+  // pieces does not matter): a wave whose weight rows are all zero-padding
+  // columns (>= ns + nf) loads none of them -- their fragments are never read
+  const bool b_dead = EMODE == 2 && SB == 2 && n0 + wave * (BN / NW) >= p.ns + p.nf;
   auto issue_b = [&](int k) {          // B of K-step k (TPS taps of one chunk) into stage k % SB
+    if (b_dead) return;
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
       const int sk = k * TPS + u, c = sk / NTAP, t = sk - c * NTAP;
@@ -1747,7 +1764,9 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
   if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
   a.wt_bytes = (int)wt_bytes;
   a.m_off = 0;
-  a.stagger = 0;
+  // KPD_KH_STAGGER=1 (A/B): waves 4-7 issue their DMA pieces one pass later
+  static const bool kh_stagger = kpd_diag_env("KPD_KH_STAGGER") != nullptr;
+  a.stagger = kh_stagger ? 1 : 0;
   // one launch for all ROIs (the kernel's input descriptor is per tile); the
   // GEMM row index stays a 32-bit int
   if ((long)a0.R * HPP >= 0x7fffffffL) return hipErrorInvalidValue;
@@ -1773,7 +1792,7 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
       else hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 32, 1, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
     } else {
       if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 2, 0, BM, true, 128, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
-      else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 64, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
       else hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 32, 3, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
     }
     const hipError_t e = hipGetLastError();
@@ -1957,6 +1976,13 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   // evict the weights and input rows from L2), -1 % time
   static const int out_nt = kpd_diag_env("KPD_FPN0X_NT") ? atoi(kpd_diag_env("KPD_FPN0X_NT")) : 1;
   b.out_nt = out_nt;
+  // class-half tile order (the kernel's tile_at); KPD_FPN0X_ORDER=0: class-fastest rounds (A/B)
+  static const int order = kpd_diag_env("KPD_FPN0X_ORDER") ? atoi(kpd_diag_env("KPD_FPN0X_ORDER")) : 1;
+  // (every round must give each workgroup a tile until the last, so the
+  // (image, row block) count must fill whole pairs of rounds: NJ a multiple
+  // of grid / 8 and at least one pair)
+  const long NJ = (long)a.N * a.tpc;
+  b.order = (order && grid % 8 == 0 && NJ % (grid / 8) == 0 && NJ >= grid / 8) ? 1 : 0;
 #if KPD_DIAG   // ablations (KPD_FPN0X_DBG=1: no MFMA, 2: no K-loop DMA, 4: one output piece); wrong results by design
   if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, b);

@@ -120,6 +120,7 @@ struct Fpn0xArgs {
   int f_bytes, l_bytes, w0_bytes, weff_bytes;
   int stagger;             // launcher: waves 4-7 issue their K-loop DMA one pass later
   int out_nt;              // launcher: non-temporal output stores
+  int order;               // launcher: 1 = class-half tile order (grid % 8 == 0), 0 = class-fastest rounds
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
   // footprint stores (boxes != null): image n's output pixels are stored only
   // inside the rectangle its ROI aligns read -- the union over its fp_P

@@ -224,7 +224,9 @@ def main():
         line["roofline"] = roof
         kh = bd.get("keypoint_head")
         if kh:
-            line["keypoint_head_tflops"] = round(fl["keypoint_head"] * c["B"] / nl / (kh[0] * 1e-3) / 1e12, 2)
+            # the spatial attention's 1x1 convs run fused in the roi_align stage (roi_kh_kernel) unless fp32
+            kf = fl["keypoint_head"] if a.precision == "fp32" else fl["keypoint_head_convs"]
+            line["keypoint_head_tflops"] = round(kf * c["B"] / nl / (kh[0] * 1e-3) / 1e12, 2)
         if a.cpu_sample > 0:
             ci = bench.host_cpu_info()
             S = min(a.cpu_sample, c["B"])

@@ -110,6 +110,11 @@ print(sys.argv[2], "value", c["value"], "ms", c["ms_per_step"], {k: round(v, 3) 
 PY
       done
     done ;;
+  grad)
+    # K6 backward timing at the heatmap conv 2 shape
+    timeout -k 10 300 python3 tools/bench_conv3_grad.py --rois 64 > "$OUT/conv3_grad.json" 2> "$OUT/grad.err" \
+      || { echo "grad rc=$?"; tail -5 "$OUT/grad.err"; exit 1; }
+    cut -c1-600 "$OUT/conv3_grad.json" ;;
   *) echo "unknown step $S"; exit 1 ;;
   esac
 done
