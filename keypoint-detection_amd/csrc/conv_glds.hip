@@ -1096,9 +1096,20 @@ constexpr int AWIN = 384;               // A window rows per chunk
 // NTAP (MODE 2): 10 = the 3x3 taps plus the ResidualBlock's 1x1 downsample as
 // a tenth K-step per chunk (the centre tap's A rows, its own weights) into a
 // second accumulator set.
-template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false,
-          int NW = 8, int MODE = -1, int NTAP = 9>
-__global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
+template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE>
+constexpr int hmconv_lds_bytes() {
+  constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
+  constexpr int RING = 2 * AWIN * ROWB + SB * BN * ROWB * TPS;
+  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH, 128, NW * 64>();
+  return RING > EPI ? RING : EPI;
+}
+
+// One tile: logical tile L of the launch's tile space, rows from padded
+// position HP + m_off + (L / (cout / BN)) * BMH; lds: the workgroup's LDS
+// (hmconv_lds_bytes), declared by the calling kernel so that kernels running
+// tiles of two heights (hmconv_mixed_kernel) share one allocation.
+template <int BN, int SB, int DBG, int BMH, bool SPLIT, int CIN, int TPS, bool DB, int NW, int MODE, int NTAP>
+__device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, const int L, const int m_off) {
   constexpr int NTH = NW * 64;
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
   static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB), "tenth tap: KH downsample");
@@ -1110,21 +1121,17 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   constexpr int A_LD = AWIN / 8 / NW;                    // A-window DMA wave-instructions per wave (6, NW 4: 12)
   constexpr int B_LD = BN / 8 / NW;                      // B DMA wave-instructions per wave per K-step
   constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
-  constexpr int RING = 2 * ABUF + SB * BSTAGE;   // A windows double-buffered, SB-stage weight ring
   static_assert(TPS == 1 || (SPLIT && NTAP % TPS == 0), "taps per step");
   constexpr bool FINAL = EMODE == 1;
-  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH, 128, NTH>();
-  constexpr int LDS = RING > EPI ? RING : EPI;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+  static_assert(hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE>() <= 160 * 1024, "LDS budget");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // KH mode: column groups by wave halves (waves w and w + 4 share a SIMD, so
   // a group with fewer live columns pairs with a full one on every SIMD)
   const int wm = EMODE == 2 ? wave % WAVES_M : wave / WAVES_N, wn = EMODE == 2 ? wave / WAVES_M : wave % WAVES_N;
   const int NTL = p.cout / BN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = HP + p.m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
+  const int m0 = HP + m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
+  if (m0 >= p.R * HPP - HP) return;   // (a padding tile of hmconv_mixed_kernel's tail)
   // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
   // channels as [hi32 | lo32] f16
   const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = NTAP * NC;
@@ -1698,6 +1705,48 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
   }
 }
 
+template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false,
+          int NW = 8, int MODE = -1, int NTAP = 9>
+__global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE>()];
+  hmconv_tile<BN, SB, DBG, BMH, SPLIT, CIN, TPS, DB, NW, MODE, NTAP>(p, lds, xcd_remap(blockIdx.x, gridDim.x),
+                                                                        p.m_off);
+}
+
+// Full rounds of BMH-row tiles and a last round of BMT-row tiles (the rows
+// left over), in ONE launch whose first round mixes the two: on every XCD
+// half of the first round's workgroups take a short tail tile, so those CUs
+// run a tail-tile's length ahead of the others from then on.  The epilogues
+// of a round (every CU writing its tile at once: 59 MB for heatmap conv 1 /
+// 2 at 64 ROIs, HBM-bound) then come as two half bursts instead of one.  The
+// makespan is the two-launch schedule's (each CU: full tiles + one tail).
+// mix_F full tiles and mix_H tail tiles (multiples of 8: one share per XCD);
+// per XCD x (blockIdx % 8) the blocks run in the order: mix_lead pairs (tail,
+// full), the remaining full tiles, the remaining tail tiles; tile indices
+// stay contiguous per XCD (L2 sharing of neighbouring windows, as xcd_remap).
+template <int BN, int SB, int BMH, int BMT, int CIN, int TPS, bool DB, int MODE>
+__global__ __launch_bounds__(512) void hmconv_mixed_kernel(const HmConvArgs p) {
+  constexpr int LB = hmconv_lds_bytes<BN, SB, BMH, true, TPS, 8, MODE>(),
+                LT = hmconv_lds_bytes<BN, SB, BMT, true, TPS, 8, MODE>();
+  __shared__ __attribute__((aligned(1024))) char lds[LB > LT ? LB : LT];
+  const int x = blockIdx.x % 8, k = blockIdx.x / 8;
+  const int Fx = p.mix_F / 8, Hx = p.mix_H / 8, h0 = min(Hx, p.mix_lead);
+  bool tail;
+  int idx;
+  if (k < 2 * h0) {
+    tail = (k & 1) == 0;
+    idx = k >> 1;
+  } else if (k - 2 * h0 < Fx - h0) {
+    tail = false;
+    idx = h0 + (k - 2 * h0);
+  } else {
+    tail = true;
+    idx = h0 + (k - 2 * h0 - (Fx - h0));
+  }
+  if (tail) hmconv_tile<BN, SB, 0, BMT, true, CIN, TPS, DB, 8, MODE, 9>(p, lds, x * Hx + idx, p.m_off + p.mix_F * BMH);
+  else hmconv_tile<BN, SB, 0, BMH, true, CIN, TPS, DB, 8, MODE, 9>(p, lds, x * Fx + idx, p.m_off);
+}
+
 constexpr long kMaxDesc = 0x7fffffffL;   // buffer descriptors take 31-bit extents
 
 template <bool SPLIT, typename TO, int KS, int BN, int S, bool PF = (BN <= 128)>
@@ -1764,9 +1813,11 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
   if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
   a.wt_bytes = (int)wt_bytes;
   a.m_off = 0;
-  // KPD_KH_STAGGER=1 (A/B): waves 4-7 issue their DMA pieces one pass later
-  static const bool kh_stagger = kpd_diag_env("KPD_KH_STAGGER") != nullptr;
-  a.stagger = kh_stagger ? 1 : 0;
+  // staggered DMA issue (waves 4-7 one pass later, as the heatmap convs):
+  // KEYPOINT_HEAD stage at C3 4.41 / 4.51 vs 4.53 / 4.58 ms (same-box A/B,
+  // KPD_KH_NOSTAGGER=1: off)
+  static const bool kh_nostagger = kpd_diag_env("KPD_KH_NOSTAGGER") != nullptr;
+  a.stagger = kh_nostagger ? 0 : 1;
   // one launch for all ROIs (the kernel's input descriptor is per tile); the
   // GEMM row index stays a 32-bit int
   if ((long)a0.R * HPP >= 0x7fffffffL) return hipErrorInvalidValue;
@@ -1869,8 +1920,32 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // bytes per MFMA, but one wave per SIMD hides no latency: 0.204 vs 0.173 ms
     static const bool hm3_nw4 = kpd_diag_env("KPD_HM3_NW4") != nullptr;
     a.m_off = 0;
+    // one launch for the full rounds and the tail round, the first round
+    // mixing both tile heights (hmconv_mixed_kernel).  Same-box A/B (round 4,
+    // 64 ROIs): conv 1 178 / 180 vs 183 / 182 us (it had no tail launch, so
+    // it also gains the tail tiles' packing), conv 2 502 / 504 vs 500 / 500,
+    // conv 3 182 / 185 vs 178 / 174 -- on for conv 1 only (KPD_HM_MIX=0: off,
+    // 2: conv 2 / conv 3 too)
+    static const int mix_env = kpd_diag_env("KPD_HM_MIX") ? atoi(kpd_diag_env("KPD_HM_MIX")) : 1;
+    const bool no_mix = mix_env == 0 || (mix_env == 1 && a.cin != 64);
+    auto mix_ok = [&](long F, long H) { return !no_mix && ncu % 8 == 0 && F >= ncu && H > 0 && H <= ncu; };
+    auto mix_set = [&](HmConvArgs& m, long F, long H, dim3& g) {
+      m.mix_F = (int)F;
+      m.mix_H = (int)((H + 7) / 8 * 8);   // a share per XCD; tiles past the rows return at once
+      m.mix_lead = ncu / 16;              // half of each XCD's CUs start with a tail tile
+      g = dim3((unsigned)(m.mix_F + m.mix_H));
+    };
     if (fin && !dbg && !no_tail && !a.stamps && (!split || (a.cin == 256 && hm_db))) {
       const long nfull = rows / BM, F = nfull / ncu * ncu, rem = rows - F * BM, H = (rem + 127) / 128;
+      if (split && mix_ok(F, H)) {
+        HmConvArgs m = a;
+        dim3 g;
+        mix_set(m, F, H, g);
+        hipLaunchKernelGGL((hmconv_mixed_kernel<64, 2, BM, 128, 256, 3, true, -1>), g, dim3(NT), 0, st, m);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
+      }
       if (F > 0 && H > 0 && H <= ncu) {
         const dim3 g1((unsigned)F), g2((unsigned)H);
         HmConvArgs a2 = a;
@@ -1897,6 +1972,19 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // per-tile prologue / epilogue dominate) measured 2 % slower with it.
     // Same K order per row: results unchanged.
     static const bool no_tail12 = kpd_diag_env("KPD_HM12_NOTAIL") != nullptr;   // A/B
+    if (split && !fin && bn == 256 && bm == 224 && (a.cin == 64 || a.cin == 256) && !dbg && !a.stamps) {
+      const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
+      if (mix_ok(F, H)) {   // conv 1 / conv 2
+        HmConvArgs m = a;
+        dim3 g;
+        mix_set(m, F, H, g);
+        if (a.cin == 64) hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 192, 64, 1, false, -1>), g, dim3(NT), 0, st, m);
+        else hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 192, 256, 1, false, -1>), g, dim3(NT), 0, st, m);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
+      }
+    }
     if (split && !fin && bn == 256 && bm == 224 && a.cin == 256 && !dbg && !no_tail12 && !a.stamps) {
       const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
       if (F > 0 && rem > 0 && H <= ncu) {

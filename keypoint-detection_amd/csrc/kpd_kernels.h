@@ -81,6 +81,7 @@ struct HmConvArgs {
   float* heat;
   int r0;                // first ROI of the launch chunk (launcher)
   int m_off;             // launcher: first GEMM row of tile 0 (tail launch of conv 3)
+  int mix_F, mix_H, mix_lead;   // launcher: hmconv_mixed_kernel's full / tail tile counts, lead pairs per XCD
   int in_bytes, wt_bytes;   // launcher
   int stagger;              // launcher: split K loop, waves 4-7 issue their DMA one pass later
   unsigned long long* stamps;   // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
