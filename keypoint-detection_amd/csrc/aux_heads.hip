@@ -17,6 +17,7 @@
 
 #include "kpd_common.h"
 #include "kpd_kernels.h"
+#include "conv_epilogue.h"
 
 namespace {
 constexpr int G = 56, GP = G * G, NA = 9;
@@ -65,6 +66,134 @@ __global__ __launch_bounds__(256) void person_decode_kernel(const float* __restr
   const float hh = ah * expf(fminf(h[a * 4 + 3], clip));
   *reinterpret_cast<float4*>(cand_boxes + idx * 4) = make_float4(cx, cy, w, hh);
   cand_scores[idx] = score > conf ? score : -INFINITY;
+}
+
+// The whole detector front end in one pass (replaces adaptive_pool56_kernel ->
+// the 45-column 1x1 conv -> person_decode_kernel, whose pooled [B][3136][128]
+// and head [B][3136][48] maps went through HBM).  One 512-thread workgroup per
+// (image, grid row i), XCD-contiguous in i (neighbouring rows' bins share an
+// input row, which then hits the same L2):
+//   1. column sums of the row's input rows [y0, y1) for every x and channel
+//      quad (coalesced 512-byte pixel rows, 4 rows' loads in flight per item)
+//      -> LDS [Wf][128];
+//   2. bins: sum of the column sums over [x0, x1), / count (adaptive-avg-pool
+//      bins; the sum runs over columns of row sums instead of row-major);
+//   3. box_heads[0] ++ cls_heads[0] on v_mfma_f32_16x16x4_f32 (exact fp32
+//      products), waves 0-3: columns 0-31 of bin block w, 4-7: columns 32-47;
+//   4. the row's 504 anchors decoded as person_decode_kernel does.
+// in: FPN level 0 [B][Hf][Wf][128] fp32; w: [48][128] (rows 45..47 zero), bias
+// [48].  Dynamic LDS: person_detect_lds(Wf).
+constexpr int kPdPP = 128 + 4, kPdHS = 49;
+inline size_t person_detect_lds(int Wf) {
+  return std::max<size_t>((size_t)Wf * 128 * 4, (size_t)G * kPdHS * 4) + (size_t)G * kPdPP * 4;
+}
+__global__ __launch_bounds__(512) void person_detect_kernel(const float* __restrict__ in, int Hf, int Wf,
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            const float* __restrict__ anchors, float inv_w,
+                                                            float inv_h, float conf, float* __restrict__ cand_boxes,
+                                                            float* __restrict__ cand_scores) {
+  constexpr int C = 128, PP = kPdPP, HC = 45, HS = kPdHS, NT = 512;
+  extern __shared__ __attribute__((aligned(16))) float pd_lds[];
+  float* colsum = pd_lds;                                  // [Wf][128]; later the head outputs [56][49]
+  float* pool = pd_lds + std::max(Wf * C, G * HS);         // [56][132]
+  const int L = xcd_remap(blockIdx.x, gridDim.x), b = L / G, i = L - b * G, tid = threadIdx.x;
+  const int y0 = (i * Hf) / G, y1 = ((i + 1) * Hf + G - 1) / G;
+  const float* src = in + (size_t)b * Hf * Wf * C;
+  // 1. column sums, 3 items x 4 rows of loads in flight per thread
+  for (int base = 0; base < Wf * 32; base += 3 * NT) {
+    float4 s[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ys = y0; ys < y1; ys += 4) {
+      float4 v[3][4];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int it = base + k * NT + tid, x = it >> 5, q = it & 31;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          v[k][u] = (it < Wf * 32 && ys + u < y1)
+                        ? *reinterpret_cast<const float4*>(src + ((size_t)(ys + u) * Wf + x) * C + q * 4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s[k].x += v[k][u].x; s[k].y += v[k][u].y; s[k].z += v[k][u].z; s[k].w += v[k][u].w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int it = base + k * NT + tid;
+      if (it < Wf * 32) *reinterpret_cast<float4*>(colsum + (it >> 5) * C + (it & 31) * 4) = s[k];
+    }
+  }
+  __syncthreads();
+  // 2. bins
+  for (int it = tid; it < G * 32; it += NT) {
+    const int j = it >> 5, q = it & 31;
+    const int x0 = (j * Wf) / G, x1 = ((j + 1) * Wf + G - 1) / G;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int x = x0; x < x1; ++x) {
+      const float4 v = *reinterpret_cast<const float4*>(colsum + x * C + q * 4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const float cnt = (float)((y1 - y0) * (x1 - x0));
+    *reinterpret_cast<float4*>(pool + j * PP + q * 4) = make_float4(s.x / cnt, s.y / cnt, s.z / cnt, s.w / cnt);
+  }
+  __syncthreads();
+  // 3. heads (the head outputs overwrite the dead column sums)
+  float* head = colsum;
+  {
+    const int lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+    const int rb = wave & 3, nb0 = wave < 4 ? 0 : 2, nnb = wave < 4 ? 2 : 1;
+    const int row = rb * 16 + r16;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kc = 0; kc < C / 16; ++kc) {
+      // lane (g, r16) supplies A[bin r16][16 kc + 4g .. +3] and B[col r16][same k]
+      const float4 a = row < G ? *reinterpret_cast<const float4*>(pool + row * PP + kc * 16 + g * 4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        if (n >= nnb) continue;
+        const float4 bw = *reinterpret_cast<const float4*>(w + (size_t)((nb0 + n) * 16 + r16) * C + kc * 16 + g * 4);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bw.x, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bw.y, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bw.z, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bw.w, acc[n], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = (nb0 + n) * 16 + r16;
+      if (n >= nnb || col >= HC) continue;
+      const float bb = bias[col];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = rb * 16 + g * 4 + e;   // D: lane holds rows 4g + e of its block, column r16
+        if (j < G) head[j * HS + col] = acc[n][e] + bb;
+      }
+    }
+  }
+  __syncthreads();
+  // 4. decode
+  for (int it = tid; it < G * NA; it += NT) {
+    const int j = it / NA, a = it - j * NA;
+    const float* h = head + j * HS;
+    const size_t idx = ((size_t)b * GP + i * G + j) * NA + a;
+    const int anc = (i * G + j) * NA + a;
+    const float score = kpd_sigmoid(h[36 + a]);
+    const float ax = anchors[anc * 4 + 0], ay = anchors[anc * 4 + 1];
+    const float aw = anchors[anc * 4 + 2] * inv_w, ah = anchors[anc * 4 + 3] * inv_h;
+    const float clip = 4.135166556742356f;   // log(1000/16)
+    const float cx = ax + h[a * 4 + 0] * aw;
+    const float cy = ay + h[a * 4 + 1] * ah;
+    const float bw = aw * expf(fminf(h[a * 4 + 2], clip));
+    const float bh = ah * expf(fminf(h[a * 4 + 3], clip));
+    *reinterpret_cast<float4*>(cand_boxes + idx * 4) = make_float4(cx, cy, bw, bh);
+    cand_scores[idx] = score > conf ? score : -INFINITY;
+  }
 }
 
 // x'[c] = x[c] * sigmoid(b + sum_k w[k] * sa1[k]) in place; thread per pixel.
@@ -341,6 +470,20 @@ hipError_t launch_adaptive_pool56(const float* in, int B, int Hf, int Wf, int C,
   const size_t total = (size_t)B * GP * (C / 4);
   hipLaunchKernelGGL(adaptive_pool56_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, B, Hf, Wf,
                      C, out);
+  return hipGetLastError();
+}
+
+bool person_detect_fits(int Wf) { return Wf >= 1 && person_detect_lds(Wf) <= 160 * 1024; }
+
+hipError_t launch_person_detect(const float* feat, int B, int Hf, int Wf, const float* w, const float* bias,
+                                const float* anchors, int img_h, int img_w, float conf, float* cand_boxes,
+                                float* cand_scores, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (Hf < 1 || Wf < 1 || !w || !bias || !anchors) return hipErrorInvalidValue;
+  const size_t lds = person_detect_lds(Wf);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;   // (the caller takes the unfused path)
+  hipLaunchKernelGGL(person_detect_kernel, dim3((unsigned)(B * G)), dim3(512), lds, st, feat, Hf, Wf, w, bias,
+                     anchors, 1.f / (float)img_w, 1.f / (float)img_h, conf, cand_boxes, cand_scores);
   return hipGetLastError();
 }
 

@@ -1072,7 +1072,15 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
 //   BN 64 : conv 3 with the final 1x1 64->17 + sigmoid fused (mixed mode),
 //           written to the [B][P][17][56][56] heatmap at the ROI's slot.
 constexpr int HP = 58, HPP = HP * HP;   // padded ROI side, positions per ROI
-constexpr int AWIN = 384;               // A window rows per chunk
+constexpr int AWIN = 384;               // A window rows per chunk (tiles of <= 256 rows)
+// A window rows of a BMH-row tile: 64 halo rows above, >= 64 below (a tap
+// reads rows 64 - 59 .. 64 + 59 + BMH - 1 of the window)
+template <int BMH>
+constexpr int hm_awin() { return BMH + 128 <= AWIN ? AWIN : BMH + 128; }
+// epilogue (MODE 0) row parts: a 384-row tile stages its fp32 accumulators
+// through LDS in two 192-row halves (one [384][132] tile exceeds the LDS)
+template <int BMH>
+constexpr int hm_epi_parts() { return BMH > 256 ? 2 : 1; }
 // DBG (A/B ablations, KPD_HMCONV_DBG): 1 = no MFMA, 2 = no weight / window
 // DMA inside the K loop (the prologue's still lands)
 // BMH: GEMM rows per tile (256, or 224 so that the tile count packs the CUs'
@@ -1099,8 +1107,8 @@ constexpr int AWIN = 384;               // A window rows per chunk
 template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE>
 constexpr int hmconv_lds_bytes() {
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
-  constexpr int RING = 2 * AWIN * ROWB + SB * BN * ROWB * TPS;
-  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH, 128, NW * 64>();
+  constexpr int RING = 2 * hm_awin<BMH>() * ROWB + SB * BN * ROWB * TPS;
+  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
   return RING > EPI ? RING : EPI;
 }
 
@@ -1108,24 +1116,49 @@ constexpr int hmconv_lds_bytes() {
 // position HP + m_off + (L / (cout / BN)) * BMH; lds: the workgroup's LDS
 // (hmconv_lds_bytes), declared by the calling kernel so that kernels running
 // tiles of two heights (hmconv_mixed_kernel) share one allocation.
-template <int BN, int SB, int DBG, int BMH, bool SPLIT, int CIN, int TPS, bool DB, int NW, int MODE, int NTAP>
-__device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, const int L, const int m_off) {
+// PST (persistent kernel, hmconv_persist_kernel): LDS as [A0 | B0 | A1 | B1]
+// (window buffer c & 1 beside weight stage c & 1), so that after the K loop
+// A0 + B0 take the NEXT tile's prologue (chunk 0 window, B(0): issued before
+// this tile's epilogue when next_m0 >= 0) while the epilogue stages through
+// A1 + B1 in four 112-row x 128-column parts; the epilogue's VMEM operations
+// are a fixed count per wave (buffer stores with out-of-range offsets for
+// border rows, both amax atomics always), so the next tile's first barrier
+// waits for its prologue with a counted vmcnt, not for these stores.
+// pre: this tile's prologue was issued by the previous tile.
+template <int BMH>
+constexpr int hm_pst_stores() { return 2 * 2 * ((BMH / 2 + 31) / 32) * 2; }   // parts x IT x (hi, lo)
+template <int BN, int SB, int DBG, int BMH, bool SPLIT, int CIN, int TPS, bool DB, int NW, int MODE, int NTAP,
+          bool PST = false>
+__device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, const int L, const int m_off,
+                                            const bool pre = false, const int next_m0 = -1) {
   constexpr int NTH = NW * 64;
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
   static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB), "tenth tap: KH downsample");
   static_assert(EMODE != 2 || (SPLIT && !DB), "KH epilogue: split, single fragment set");
   constexpr int WAVES_N = BN / 64, WAVES_M = NW / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
-  static_assert(WM % 16 == 0 && BMH + 128 <= AWIN, "tile rows");
+  constexpr int AW = hm_awin<BMH>();
+  static_assert(WM % 16 == 0 && BMH + 128 <= AW && AW % (8 * NW) == 0, "tile rows");
   static_assert(NW == 8 || (BN == 64 && SPLIT && DB), "4 waves: the conv 3 split DB variant only");
-  constexpr int A_LD = AWIN / 8 / NW;                    // A-window DMA wave-instructions per wave (6, NW 4: 12)
+  constexpr int A_LD = AW / 8 / NW;                      // A-window DMA wave-instructions per wave (6; 8 at 384 rows; NW 4: 12)
+  static_assert(A_LD <= 9 || TPS > 1, "window pieces: one per tap");
   constexpr int B_LD = BN / 8 / NW;                      // B DMA wave-instructions per wave per K-step
-  constexpr int ABUF = AWIN * ROWB, BSTAGE = BN * ROWB * TPS;
+  constexpr int ABUF = AW * ROWB, BSTAGE = BN * ROWB * TPS;
   static_assert(TPS == 1 || (SPLIT && NTAP % TPS == 0), "taps per step");
   constexpr bool FINAL = EMODE == 1;
   static_assert(hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE>() <= 160 * 1024, "LDS budget");
+  static_assert(!PST || (SPLIT && EMODE == 0 && SB == 2 && TPS == 1 && !DB && NW == 8 && NTAP == 9 && BN == 256 &&
+                         BMH <= 224 && DBG == 0), "persistent tiles: split conv 1 / conv 2 (BN = cout = 256)");
+  // window buffer of chunk c, weight stage s (PST: [A0 | B0 | A1 | B1])
+  auto a_at = [&](int c) { return PST ? (c & 1) * (ABUF + BSTAGE) : (c & 1) * ABUF; };
+  auto b_at = [&](int st) { return PST ? st * (ABUF + BSTAGE) + ABUF : 2 * ABUF + st * BSTAGE; };
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tid = threadIdx.x;
+  // PST: per tile, tid is opaque, so that the lane-dependent offsets are
+  // recomputed in every tile instead of hoisted out of the persistent loop
+  // and held (with the tile's own working set they overflow the registers)
+  if constexpr (PST) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wave = tid >> 6;
   // KH mode: column groups by wave halves (waves w and w + 4 share a SIMD, so
   // a group with fewer live columns pairs with a full one on every SIMD)
   const int wm = EMODE == 2 ? wave % WAVES_M : wave / WAVES_N, wn = EMODE == 2 ? wave / WAVES_M : wave % WAVES_N;
@@ -1150,7 +1183,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   unsigned a_off[A_LD];
 #pragma unroll
   for (int i = 0; i < A_LD; ++i) {
-    const int m = m0 - 64 + wave * (AWIN / NW) + i * 8 + lrow;
+    const int m = m0 - 64 + wave * (AW / NW) + i * 8 + lrow;
     a_off[i] = (m >= 0 && m < Mtot) ? (unsigned)((m - wbase) * RB + lchunk * 16) : OOB;
   }
   unsigned b_off[B_LD];
@@ -1160,7 +1193,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     b_off[i] = (unsigned)(co * NTAP * RB + lchunk * 16);
   }
   auto issue_a = [&](int c, int i) {   // A window of chunk c, wave-instruction i
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (c & 1) * ABUF + (wave * (AWIN / NW) + i * 8) * ROWB);
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + a_at(c) + (wave * (AW / NW) + i * 8) * ROWB);
     glds16(rin, dst, a_off[i] == OOB ? OOB : a_off[i] + c * 128, 0);
   };
   // KH mode, 2-stage ring (every barrier waits vmcnt(0), so a wave's count of
@@ -1172,8 +1205,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
 #pragma unroll
     for (int u = 0; u < TPS; ++u) {
       const int sk = k * TPS + u, c = sk / NTAP, t = sk - c * NTAP;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + 2 * ABUF + (k % SB) * BSTAGE + u * BN * ROWB +
-                                                          wave * (BN / NW) * ROWB);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + b_at(k % SB) + u * BN * ROWB + wave * (BN / NW) * ROWB);
 #pragma unroll
       for (int i = 0; i < B_LD; ++i) glds16(rwt, dst + i * 8 * ROWB, b_off[i], t * RB + c * 128);
     }
@@ -1205,8 +1237,8 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   // half q of K-step k: A rows shifted by the tap offset (swizzle by the row)
   auto load_half = [&](int k, int q, Half& f) {
     const int c = k / 9, t = k - c * 9, off = (t / 3 - 1) * HP + (t % 3 - 1);
-    const char* ab = lds + (c & 1) * ABUF;
-    const char* bb = lds + 2 * ABUF + (k % SB) * BSTAGE;
+    const char* ab = lds + a_at(c);
+    const char* bb = lds + b_at(k % SB);
 #pragma unroll
     for (int j = 0; j < FN; ++j) f.b[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
     const int r0w = wm * WM + r16 + 64 + off;   // window row of fragment 0 (rows of fragment i: + 16 i)
@@ -1256,12 +1288,22 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   const int rbound = (rlo + 1) * HPP;       // first padded position of the tile's second ROI
   // prologue: chunk 0's window and the first SB-1 K-steps' weights
   const int KS = KT / TPS;                  // K-steps (barriers)
+  if (!PST || !pre) {
 #pragma unroll
-  for (int i = 0; i < A_LD; ++i) issue_a(0, i);
+    for (int i = 0; i < A_LD; ++i) issue_a(0, i);
 #pragma unroll
-  for (int k = 0; k < SB - 1; ++k)
-    if (k < KS) issue_b(k);
-  barrier_k(KS < SB - 1);
+    for (int k = 0; k < SB - 1; ++k)
+      if (k < KS) issue_b(k);
+    barrier_k(KS < SB - 1);
+  } else {
+    // prologue issued by the previous tile, before its epilogue's fixed count
+    // of VMEM operations (hm_pst_stores<224> stores + 2 amax atomics)
+    if (p.amax_idx >= 0) wait_vmcnt<hm_pst_stores<224>() + 2>();
+    else wait_vmcnt<hm_pst_stores<224>()>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
   stamp16(p.stamps, 1);
   stamp16(p.stamps, 6, __builtin_amdgcn_s_memtime());   // shader clock (K-loop clock rate)
   // the next chunk's window, spread over this chunk's K-steps: pieces of
@@ -1322,7 +1364,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     uint4 ah[FM], al[FM], bh[FN], bl[FN];
     auto rd_a = [&](int k, int q, uint4* f) {
       const int c = k / NTAP, t = k - c * NTAP, off = t == 9 ? 0 : (t / 3 - 1) * HP + (t % 3 - 1);
-      const char* ab = lds + (c & 1) * ABUF;
+      const char* ab = lds + a_at(c);
       const int r0w = wm * WM + r16 + 64 + off;
       const int ach = (((q ? 4 : 0) + g) ^ (r0w & 7)) << 4;
 #pragma unroll
@@ -1361,8 +1403,8 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
       }
       struct Frag { uint4 ah[FM], al[FM], bh[FN], bl[FN]; };
       auto rd_all = [&](int c, int t, int stage, Frag& f) {
-        const char* ab = lds + (c & 1) * ABUF;
-        const char* bb = lds + 2 * ABUF + stage * BSTAGE + (t % TPS) * BN * ROWB + b_row;
+        const char* ab = lds + a_at(c);
+        const char* bb = lds + b_at(stage) + (t % TPS) * BN * ROWB + b_row;
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           f.al[i] = *reinterpret_cast<const uint4*>(ab + (aoff[t] ^ 64) + i * 16 * ROWB);
@@ -1406,7 +1448,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     auto run_loop = [&](auto NBc, auto NMc, auto NM9c) {
       constexpr int NB_ = decltype(NBc)::value;
       auto rd_bn = [&](int k, int q, uint4* f) {
-        const char* bb = lds + 2 * ABUF + ((k / TPS) % SB) * BSTAGE + (k % TPS) * BN * ROWB;
+        const char* bb = lds + b_at((k / TPS) % SB) + (k % TPS) * BN * ROWB;
 #pragma unroll
         for (int j = 0; j < NB_; ++j)
           f[j] = *reinterpret_cast<const uint4*>(bb + b_row + j * 16 * ROWB + (q ? bch1 : bch0));
@@ -1492,6 +1534,40 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   stamp16(p.stamps, 7, __builtin_amdgcn_s_memtime());
   __syncthreads();
   stamp16(p.stamps, 2);
+  float pbias[PST ? 2 : 1][8];
+  if constexpr (PST) {
+    // the loads of this tile are consumed here (no compiler wait lands behind
+    // the prefetch below)
+    // the epilogue's bias (this thread's 8 channels of each 128-column half)
+    // is read before the prefetch too (L2 hits, ~0.4 us)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int co = n0 + h * 128 + (tid % 16) * 8;
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + co);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + co + 4);
+      pbias[h][0] = b0.x; pbias[h][1] = b0.y; pbias[h][2] = b0.z; pbias[h][3] = b0.w;
+      pbias[h][4] = b1.x; pbias[h][5] = b1.y; pbias[h][6] = b1.z; pbias[h][7] = b1.w;
+    }
+    asm volatile("" ::"v"(us[0]), "v"(us[1]), "v"(os[0]), "v"(os[1]));
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(pbias[h][e]));
+    // the next tile's prologue into A0 / B0 (free: the last K-step used A1 / B1)
+    if (next_m0 >= 0) {
+      const int nwb = max(next_m0 - 64, 0);
+      const i32x4 nrin = make_rsrc(static_cast<const char*>(p.in) + (size_t)nwb * RB,
+                                   (int)min(((long)Mtot - nwb) * RB, 0x7fffffffL));
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const int m = next_m0 - 64 + wave * (AW / NW) + i * 8 + lrow;
+        const unsigned off = (m >= 0 && m < Mtot) ? (unsigned)((m - nwb) * RB + lchunk * 16) : OOB;
+        const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + a_at(0) + (wave * (AW / NW) + i * 8) * ROWB);
+        glds16(nrin, dst, off, 0);
+      }
+      issue_b(0);
+    }
+  }
 
   // interior test of a padded position: ROI row/column 1..56
   auto interior = [&](int m, int& r, int& yy, int& xx) {
@@ -1501,7 +1577,64 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     xx = rem - (yy + 1) * HP - 1;
     return m < Mtot - HP && yy >= 0 && yy < HP - 2 && xx >= 0 && xx < HP - 2;
   };
-  if constexpr (EMODE == 0) {
+  if constexpr (PST) {
+    // four parts of 112 rows x 128 columns staged through A1 + B1; every
+    // wave issues exactly hm_pst_stores<BMH>() stores (border / out-of-tile
+    // rows to an out-of-range offset) and, with amax, two atomics
+    float* tile = reinterpret_cast<float*>(lds + ABUF + BSTAGE);
+    constexpr int P4 = 128 + 4, C8 = 16, RS = NTH / C8, IT = (WM + RS - 1) / RS;
+    static_assert(WAVES_M == 2 && WM * P4 * 4 <= ABUF + BSTAGE && 4 * IT * 2 == hm_pst_stores<BMH>(), "PST epilogue");
+    const int obytes = p.cout * 4;
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(p.out) + (size_t)m0 * obytes,
+                                                                          (short)0, BMH * obytes, 0x00020000);
+    float mx[2] = {0.f, 0.f};
+    const int c8 = tid % C8, row0 = tid / C8;
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      const int pr = pp >> 1, h = pp & 1;
+      if (pp) __syncthreads();
+      if (wn / 2 == h && wm == pr) acc_to_lds<FM, FN, WM, 64, 128>(tile, acc, 0, wn % 2, lane);
+      __syncthreads();
+      const int co = n0 + h * 128 + c8 * 8;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int row = row0 + it * RS, m = m0 + pr * WM + row;
+        int r, yy, xx;
+        const bool ok = row < WM && interior(m, r, yy, xx);
+        const float4 x0 = *reinterpret_cast<const float4*>(tile + min(row, WM - 1) * P4 + c8 * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(tile + min(row, WM - 1) * P4 + c8 * 8 + 4);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const int q = m >= rbound;
+        const float u = q ? us[1] : us[0], sc = q ? os[1] : os[0];
+        f16x8 hi, lo;
+        float mc = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = fmaxf(fmaf(xv[e], u, pbias[h][e]), 0.f);
+          mc = fmaxf(mc, v);
+          const float xs = v * sc;
+          hi[e] = (_Float16)xs;
+          lo[e] = (_Float16)(xs - (float)hi[e]);
+        }
+        const unsigned off = ok ? (unsigned)((m - m0) * obytes + (co >> 5) * 128 + (co & 31) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rout, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rout, ok ? off + 64 : OOB, 0, 0);
+        if (ok) {
+          if (q) mx[1] = fmaxf(mx[1], mc); else mx[0] = fmaxf(mx[0], mc);
+        }
+      }
+    }
+    if (p.amax_idx >= 0) {   // per-ROI max|out| for the next conv's output scale: two atomics per wave, always
+      const float w0 = wave_max(mx[0]), w1 = wave_max(mx[1]);
+      if (lane == 0) {
+        const bool two = rlo + 1 < p.R;
+        unsigned* a0 = reinterpret_cast<unsigned*>(p.hsc + (size_t)(p.r0 + rlo) * 4 + p.amax_idx);
+        unsigned* a1 = reinterpret_cast<unsigned*>(p.hsc + (size_t)(p.r0 + rlo + (two ? 1 : 0)) * 4 + p.amax_idx);
+        atomicMax(a0, __float_as_uint(w0));
+        atomicMax(a1, __float_as_uint(two ? w1 : 0.f));
+      }
+    }
+  } else if constexpr (EMODE == 0) {
     // bias + ReLU through the LDS tile (two 128-column halves): bf16 16-byte
     // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
     // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
@@ -1509,13 +1642,17 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     // a thread takes 8 consecutive channels of a row: 16-byte stores (the
     // epilogue's store tail is issue-bound when every CU stores at once:
     // half the store instructions of 8-byte pieces)
-    constexpr int P4 = 128 + 4, C8 = 16, RS = NTH / C8, IT = (BMH + RS - 1) / RS;
+    // (RP row parts of BR rows: the waves of part pr stage, all threads store)
+    constexpr int RP = hm_epi_parts<BMH>(), BR = BMH / RP, WPR = WAVES_M / RP;
+    static_assert(WAVES_M % RP == 0, "epilogue row parts");
+    constexpr int P4 = 128 + 4, C8 = 16, RS = NTH / C8, IT = (BR + RS - 1) / RS;
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
     float mx[2] = {0.f, 0.f};   // SPLIT: max|out| of the tile's two ROIs (>= 0 after ReLU)
 #pragma unroll
-    for (int h = 0; h < BN / 128; ++h) {
-      if (h) __syncthreads();
-      if (wn / 2 == h) acc_to_lds<FM, FN, WM, 64, 128>(tile, acc, wm, wn % 2, lane);
+    for (int ph = 0; ph < RP * (BN / 128); ++ph) {
+      const int pr = ph / (BN / 128), h = ph % (BN / 128);
+      if (ph) __syncthreads();
+      if (wn / 2 == h && wm / WPR == pr) acc_to_lds<FM, FN, WM, 64, 128>(tile, acc, wm % WPR, wn % 2, lane);
       __syncthreads();
       const int c8 = tid % C8, row0 = tid / C8, co = n0 + h * 128 + c8 * 8;
       const float4 b0 = *reinterpret_cast<const float4*>(p.bias + co);
@@ -1523,9 +1660,9 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
       const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const int row = row0 + it * RS, m = m0 + row;
+        const int row = row0 + it * RS, m = m0 + pr * BR + row;
         int r, yy, xx;
-        if (row >= BMH || !interior(m, r, yy, xx)) continue;
+        if (row >= BR || !interior(m, r, yy, xx)) continue;
         const float4 x0 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8);
         const float4 x1 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8 + 4);
         float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -1713,6 +1850,51 @@ __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
                                                                         p.m_off);
 }
 
+// Persistent heatmap conv 1 / conv 2 (split, BN = cout = 256): one
+// workgroup per CU walks full 224-row tiles t = w, w + G, ... (w: the
+// XCD-contiguous rank of the workgroup, as xcd_remap) and then tail tile w of
+// 192 rows if w < mix_H; each tile issues the next one's prologue (chunk 0
+// window + B(0)) before its epilogue (hmconv_tile PST).  mix_F full tiles
+// (whole rounds), mix_H tail tiles (exact count, <= G).
+// the kernel's argument block re-read from the kernarg segment (scalar loads;
+// the asm hides the pointer's provenance so that nothing is kept live across
+// a persistent loop's iterations)
+template <typename T>
+__device__ __forceinline__ void kernarg_copy(T& dst) {
+  typedef const __attribute__((address_space(4))) unsigned* KaPtr;
+  KaPtr ka = (KaPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ka));
+  static_assert(sizeof(T) % 4 == 0, "argument block");
+  unsigned* d = reinterpret_cast<unsigned*>(&dst);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = ka[i];
+}
+
+template <int CIN>
+__global__ __launch_bounds__(512) void hmconv_persist_kernel(const HmConvArgs p) {
+  __shared__ __attribute__((aligned(1024))) char lds[hmconv_lds_bytes<256, 2, 224, true, 1, 8, -1>()];
+  const int G = gridDim.x, w = xcd_remap(blockIdx.x, G);
+  const int F = p.mix_F, H = p.mix_H, tail_off = p.m_off + F * 224;
+  bool pre = false;
+  for (int t = w; t < F; t += G) {
+    // the arguments are re-read from the kernarg segment every tile (scalar
+    // loads) instead of held in SGPRs across the loop: the held copy pushed
+    // the tile body past the register budget (spills)
+    HmConvArgs pl;
+    kernarg_copy(pl);
+    const int nt = t + G;
+    const int next_m0 = nt < F ? HP + pl.m_off + nt * 224 : (w < H ? HP + tail_off + w * 192 : -1);
+    hmconv_tile<256, 2, 0, 224, true, CIN, 1, false, 8, -1, 9, true>(pl, lds, t, pl.m_off, pre, next_m0);
+    pre = next_m0 >= 0;
+  }
+  if (w < H) {
+    HmConvArgs pl;
+    kernarg_copy(pl);
+    hmconv_tile<256, 2, 0, 192, true, CIN, 1, false, 8, -1, 9, true>(pl, lds, w, tail_off, pre, -1);
+  }
+  wait_vmcnt<0>();
+}
+
 // Full rounds of BMH-row tiles and a last round of BMT-row tiles (the rows
 // left over), in ONE launch whose first round mixes the two: on every XCD
 // half of the first round's workgroups take a short tail tile, so those CUs
@@ -1743,7 +1925,9 @@ __global__ __launch_bounds__(512) void hmconv_mixed_kernel(const HmConvArgs p) {
     tail = true;
     idx = h0 + (k - 2 * h0 - (Fx - h0));
   }
-  if (tail) hmconv_tile<BN, SB, 0, BMT, true, CIN, TPS, DB, 8, MODE, 9>(p, lds, x * Hx + idx, p.m_off + p.mix_F * BMH);
+  // (tile indices count M-tiles x column tiles: the full tiles cover mix_F / NTL M-tiles)
+  if (tail) hmconv_tile<BN, SB, 0, BMT, true, CIN, TPS, DB, 8, MODE, 9>(p, lds, x * Hx + idx,
+                                                                       p.m_off + (p.mix_F / (p.cout / BN)) * BMH);
   else hmconv_tile<BN, SB, 0, BMH, true, CIN, TPS, DB, 8, MODE, 9>(p, lds, x * Fx + idx, p.m_off);
 }
 
@@ -1972,6 +2156,27 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     // per-tile prologue / epilogue dominate) measured 2 % slower with it.
     // Same K order per row: results unchanged.
     static const bool no_tail12 = kpd_diag_env("KPD_HM12_NOTAIL") != nullptr;   // A/B
+#if KPD_DIAG
+    // A/B (KPD_HM_PERSIST=1): conv 1 / conv 2 persistent (hmconv_persist_kernel:
+    // each tile's successor prologue issued under its epilogue).  Same-box
+    // (round 4, 64 ROIs): conv 1 0.206 vs 0.174 ms, conv 2 0.503 vs 0.504 ms
+    // -- not on by default
+    static const int persist_env = kpd_diag_env("KPD_HM_PERSIST") ? atoi(kpd_diag_env("KPD_HM_PERSIST")) : 0;
+    if (split && !fin && bn == 256 && bm == 224 && a.cout == 256 && (a.cin == 64 || a.cin == 256) && !dbg &&
+        !a.stamps && persist_env) {
+      const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
+      if (F > 0 && H <= ncu && F + H < 0x7fffffffL / 224) {
+        HmConvArgs m = a;
+        m.mix_F = (int)F;
+        m.mix_H = (int)H;
+        if (a.cin == 64) hipLaunchKernelGGL((hmconv_persist_kernel<64>), dim3((unsigned)ncu), dim3(NT), 0, st, m);
+        else hipLaunchKernelGGL((hmconv_persist_kernel<256>), dim3((unsigned)ncu), dim3(NT), 0, st, m);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
+      }
+    }
+#endif
     if (split && !fin && bn == 256 && bm == 224 && (a.cin == 64 || a.cin == 256) && !dbg && !a.stamps) {
       const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
       if (mix_ok(F, H)) {   // conv 1 / conv 2

@@ -300,6 +300,12 @@ size_t nms_scratch_bytes(int n);
 
 // ---- person-detector glue + KEYPOINT_HEAD (aux_heads.hip) ----
 hipError_t launch_adaptive_pool56(const float* in, int B, int Hf, int Wf, int C, float* out, hipStream_t st);
+// adaptive pool + 1x1 heads (w [48][128] fp32, bias [48]) + decode in one launch (the default detector path;
+// level-0 widths with person_detect_fits(Wf): the column sums fit the LDS)
+bool person_detect_fits(int Wf);
+hipError_t launch_person_detect(const float* feat, int B, int Hf, int Wf, const float* w, const float* bias,
+                                const float* anchors, int img_h, int img_w, float conf, float* cand_boxes,
+                                float* cand_scores, hipStream_t st);
 hipError_t launch_person_decode(const float* head, int B, int hc, const float* anchors, int img_h, int img_w,
                                 float conf, float* cand_boxes, float* cand_scores, hipStream_t st);
 hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st);

@@ -1645,12 +1645,21 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   // ---------------- person-detector glue (boxes become an output) ----------------
   if (detect) {
     Stage sg(p, "person_detect", st);
-    HIP_TRY(launch_adaptive_pool56(w.feat, B, d.Hf, d.Wf, 128, w.pd_pool, st));
-    if (int rc = conv(p->pd, w.pd_pool, B, 56, 56, 128, w.pd_head, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0,
-                      st))
-      return rc;
-    HIP_TRY(launch_person_decode(w.pd_head, B, p->pd.cout_p, p->anchors, H, W, p->det_conf, w.pd_boxes,
-                                 w.pd_scores, st));
+    // pool + heads + decode in one launch (person_detect_kernel); KPD_PD_UNFUSED=1:
+    // the three launches with the pooled / head maps through HBM (A/B)
+    static const bool pd_unfused = kpd_diag_env("KPD_PD_UNFUSED") != nullptr;
+    if (!pd_unfused && p->pd.cin == 128 && p->pd.cin_p == 128 && p->pd.cout_p == 48 && !p->pd.bf16 &&
+        person_detect_fits(d.Wf)) {
+      HIP_TRY(launch_person_detect(w.feat, B, d.Hf, d.Wf, static_cast<const float*>(p->pd.w), p->pd.b, p->anchors, H,
+                                   W, p->det_conf, w.pd_boxes, w.pd_scores, st));
+    } else {
+      HIP_TRY(launch_adaptive_pool56(w.feat, B, d.Hf, d.Wf, 128, w.pd_pool, st));
+      if (int rc = conv(p->pd, w.pd_pool, B, 56, 56, 128, w.pd_head, ACT_NONE, nullptr, 0, 0, nullptr, nullptr, 0, 0,
+                        st))
+        return rc;
+      HIP_TRY(launch_person_decode(w.pd_head, B, p->pd.cout_p, p->anchors, H, W, p->det_conf, w.pd_boxes,
+                                   w.pd_scores, st));
+    }
     HIP_TRY(launch_nms_sets(w.pd_boxes, w.pd_scores, B, 56 * 56 * 9, p->det_iou, P, P, w.pd_keep, w.pd_nkeep,
                             w.pd_alive, st, 1, boxes, box_scores));
   }

@@ -108,6 +108,110 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
   }
 }
 
+// Register-resident variant for n <= 1024 * 32 (the detector glue: 28,224
+// candidates per image).  Thread t owns candidates t + 1024 k: their scores
+// live in registers, their alive flags in one 32-bit mask, and each round is
+// ONE pass that applies the previous round's suppression (IoU against the box
+// kept last) and finds the best survivor at the same time -- the same
+// keep-best / drop-IoU>thr sequence as nms_kernel (same IoU arithmetic and
+// tie-break), without its global alive array and two sweeps per kept box.
+constexpr int kNmsRegSlots = 32;
+__global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__ boxes,
+                                                       const float* __restrict__ scores, int n, float thr,
+                                                       int max_out, int max_keep, int32_t* __restrict__ keep,
+                                                       int32_t* __restrict__ n_keep, int filter,
+                                                       float* __restrict__ out_boxes, float* __restrict__ out_scores) {
+  __shared__ float ws[16];
+  __shared__ int wi[16];
+  __shared__ int best_s;
+  const int set = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* bx = boxes + (size_t)set * n * 4;
+  const float* sc = scores + (size_t)set * n;
+  float s[kNmsRegSlots];
+  unsigned alive = 0u;
+#pragma unroll
+  for (int k = 0; k < kNmsRegSlots; ++k) {
+    const int i = tid + k * 1024;
+    s[k] = -INFINITY;
+    if (i < n) {
+      s[k] = sc[i];
+      if (!filter || s[k] > -INFINITY) alive |= 1u << k;
+    }
+  }
+  int kept = 0;
+  const int limit = max_out > 0 ? min(max_out, max_keep) : max_keep;
+  float kb[4] = {0.f, 0.f, 0.f, 0.f};
+  bool have_kb = false;
+  while (kept < limit) {
+    float bs = -INFINITY;
+    int bi = 0x7fffffff;
+    // groups of 8 slots: the group's box loads are all issued before its IoUs
+#pragma unroll
+    for (int k0 = 0; k0 < kNmsRegSlots; k0 += 8) {
+      if (!((alive >> k0) & 0xffu)) continue;
+      float4 v[8];
+      if (have_kb) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if ((alive >> (k0 + u)) & 1u) v[u] = *reinterpret_cast<const float4*>(bx + (size_t)(tid + (k0 + u) * 1024) * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        if (!((alive >> k) & 1u)) continue;
+        const int i = tid + k * 1024;
+        if (have_kb) {
+          const float bb[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          if (!(iou_cxcywh(kb, bb) <= thr)) {
+            alive &= ~(1u << k);
+            continue;
+          }
+        }
+        if (better(s[k], i, bs, bi)) { bs = s[k]; bi = i; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) { ws[wave] = bs; wi[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float sb = ws[0];
+      int b = wi[0];
+      for (int w = 1; w < 16; ++w)
+        if (better(ws[w], wi[w], sb, b)) { sb = ws[w]; b = wi[w]; }
+      best_s = b;
+    }
+    __syncthreads();
+    const int b = best_s;
+    if (b == 0x7fffffff) break;   // nothing alive
+    if (tid == 0) keep[(size_t)set * max_keep + kept] = b;
+    ++kept;
+    if ((b & 1023) == tid) alive &= ~(1u << (b >> 10));   // the kept box leaves the candidates
+    const float4 v = *reinterpret_cast<const float4*>(bx + (size_t)b * 4);
+    kb[0] = v.x; kb[1] = v.y; kb[2] = v.z; kb[3] = v.w;
+    have_kb = true;
+  }
+  if (tid == 0) n_keep[set] = kept;
+  if (out_boxes) {   // kept boxes, zero padded to max_keep (zero boxes are skipped downstream)
+    __syncthreads();
+    for (int t = tid; t < max_keep; t += 1024) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float sv = 0.f;
+      if (t < kept) {
+        const int k = keep[(size_t)set * max_keep + t];
+        v = *reinterpret_cast<const float4*>(bx + (size_t)k * 4);
+        sv = sc[k];
+      }
+      *reinterpret_cast<float4*>(out_boxes + ((size_t)set * max_keep + t) * 4) = v;
+      if (out_scores) out_scores[(size_t)set * max_keep + t] = sv;
+    }
+  }
+}
+
 }  // namespace
 
 size_t nms_scratch_bytes(int n) { return (size_t)n; }
@@ -118,8 +222,14 @@ hipError_t launch_nms_sets(const float* boxes, const float* scores, int sets, in
   if (n <= 0) {
     return hipMemsetAsync(n_keep, 0, sizeof(int32_t) * sets, st);
   }
-  hipLaunchKernelGGL(nms_kernel, dim3(sets), dim3(1024), 0, st, boxes, scores, n, thr, max_out, max_keep, keep,
-                     n_keep, reinterpret_cast<uint8_t*>(scratch), filter, out_boxes, out_scores);
+  // KPD_NMS_SWEEP=1: the two-sweep kernel with the global alive array for every n (A/B)
+  static const bool sweep = kpd_diag_env("KPD_NMS_SWEEP") != nullptr;
+  if (n <= 1024 * kNmsRegSlots && !sweep)
+    hipLaunchKernelGGL(nms_reg_kernel, dim3(sets), dim3(1024), 0, st, boxes, scores, n, thr, max_out, max_keep, keep,
+                       n_keep, filter, out_boxes, out_scores);
+  else
+    hipLaunchKernelGGL(nms_kernel, dim3(sets), dim3(1024), 0, st, boxes, scores, n, thr, max_out, max_keep, keep,
+                       n_keep, reinterpret_cast<uint8_t*>(scratch), filter, out_boxes, out_scores);
   return hipGetLastError();
 }
 
