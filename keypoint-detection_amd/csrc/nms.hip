@@ -116,6 +116,8 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
 // keep-best / drop-IoU>thr sequence as nms_kernel (same IoU arithmetic and
 // tie-break), without its global alive array and two sweeps per kept box.
 constexpr int kNmsRegSlots = 32;
+constexpr int kNmsPrefix = 1024;   // target size of the fast path's prefix S
+constexpr int kNmsList = 2048;     // LDS list capacity for S (ties at its threshold included)
 __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__ boxes,
                                                        const float* __restrict__ scores, int n, float thr,
                                                        int max_out, int max_keep, int32_t* __restrict__ keep,
@@ -140,23 +142,202 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
   }
   int kept = 0;
   const int limit = max_out > 0 ? min(max_out, max_keep) : max_keep;
+  // ---- fast path: greedy NMS on a prefix of the (score desc, index asc)
+  // order.  Every decision about a candidate depends only on the candidates
+  // ranked above it, so once `limit` boxes are kept inside a prefix S (all
+  // candidates whose sortable score key is >= tau), the full pass would keep
+  // the same boxes.  S: radix select of the kNmsPrefix-th largest key (8-bit
+  // digits, LDS histograms), ties at tau included while S fits the LDS list.
+  // If S runs dry before `limit` and does not hold every alive candidate, the
+  // full register pass below runs from the start.
+  {
+    __shared__ unsigned hist[16 * 257];   // per-wave histograms (stride 257: each wave's bins on other banks)
+    __shared__ unsigned sh_prefix, sh_need, sh_total;
+    __shared__ int sh_cnt;
+    __shared__ int l_idx[kNmsList];
+    __shared__ float l_sc[kNmsList];
+    auto key_of = [](float x) {   // order-preserving map of a float to unsigned (every alive key >= 0x007fffff)
+      const unsigned b = __float_as_uint(x);
+      return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    };
+    if (tid == 0) { sh_total = 0u; sh_cnt = 0; sh_prefix = 0u; sh_need = kNmsPrefix; }
+    __syncthreads();
+    {
+      unsigned c = __popc(alive);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0) atomicAdd(&sh_total, c);
+    }
+    __syncthreads();
+    const unsigned total = sh_total;
+    unsigned tau = 0u;                      // S = alive keys >= tau (0: every alive candidate)
+    if (total > (unsigned)kNmsPrefix) {
+      unsigned mask = 0u;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 16 * 257; i += 1024) hist[i] = 0u;
+        __syncthreads();
+        const unsigned prefix = sh_prefix;
+        unsigned* wh = hist + wave * 257;
+#pragma unroll
+        for (int k = 0; k < kNmsRegSlots; ++k) {
+          if (!((alive >> k) & 1u)) continue;
+          const unsigned key = key_of(s[k]);
+          if ((key & mask) == prefix) atomicAdd(&wh[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 256) {   // merge the wave histograms into wave 0's
+          unsigned c = 0u;
+          for (int w = 0; w < 16; ++w) c += hist[w * 257 + tid];
+          hist[tid] = c;
+        }
+        __syncthreads();
+        if (wave == 0) {
+          // the digit holding the need-th largest key: lane l sums bins
+          // 255 - 4l .. 252 - 4l, a wave prefix sum over the lanes (descending
+          // bins) finds the lane, then its four bins
+          unsigned c[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) c[j] = hist[255 - (4 * lane + j)];
+          const unsigned tot = c[0] + c[1] + c[2] + c[3];
+          unsigned pre = tot;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const unsigned v = __shfl_up(pre, o, 64);
+            if (lane >= o) pre += v;
+          }
+          const unsigned need = sh_need, excl = pre - tot;
+          if (excl < need && pre >= need) {
+            unsigned r = need - excl;
+            int j = 0;
+            for (; j < 3; ++j) {
+              if (r <= c[j]) break;
+              r -= c[j];
+            }
+            sh_prefix = prefix | ((unsigned)(255 - (4 * lane + j)) << shift);
+            sh_need = r;
+          }
+        }
+        mask |= 0xffu << shift;
+        __syncthreads();
+      }
+      tau = sh_prefix;                      // the kNmsPrefix-th largest key
+    }
+    // compact S into the LDS list (ties at tau too, while they fit)
+    for (int pass = 0; pass < 2; ++pass) {   // pass 0: keys > tau, pass 1: keys == tau
+#pragma unroll
+      for (int k = 0; k < kNmsRegSlots; ++k) {
+        if (!((alive >> k) & 1u)) continue;
+        const unsigned key = key_of(s[k]);
+        const bool in = pass == 0 ? (tau == 0u || key > tau) : (tau != 0u && key == tau);
+        if (!in) continue;
+        const int pos = atomicAdd(&sh_cnt, 1);
+        if (pos < kNmsList) { l_idx[pos] = tid + k * 1024; l_sc[pos] = s[k]; }
+      }
+      __syncthreads();
+      if (pass == 0 && sh_cnt > kNmsList) break;   // (cannot happen: keys > tau number < kNmsPrefix)
+    }
+    int m = sh_cnt;
+    const bool all = m == (int)total;           // S holds every alive candidate
+    if (m > kNmsList) {                         // the ties overflowed: keep only keys > tau (a prefix too)
+      __syncthreads();
+      if (tid == 0) sh_cnt = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kNmsRegSlots; ++k) {
+        if (!((alive >> k) & 1u)) continue;
+        if (!(key_of(s[k]) > tau)) continue;
+        const int pos = atomicAdd(&sh_cnt, 1);
+        l_idx[pos] = tid + k * 1024;
+        l_sc[pos] = s[k];
+      }
+      __syncthreads();
+      m = sh_cnt;
+    }
+    const bool covered = all && m <= kNmsList;
+    // greedy rounds over the list: thread t holds entries t and t + 1024
+    constexpr int PER = kNmsList / 1024;
+    int li[PER];
+    float ls[PER];
+    float4 lb[PER];
+    unsigned la = 0u;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + u * 1024;
+      li[u] = 0x7fffffff;
+      ls[u] = -INFINITY;
+      lb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < m) {
+        li[u] = l_idx[e];
+        ls[u] = l_sc[e];
+        lb[u] = *reinterpret_cast<const float4*>(bx + (size_t)li[u] * 4);
+        la |= 1u << u;
+      }
+    }
+    bool have = false;
+    float fb[4] = {0.f, 0.f, 0.f, 0.f};
+    int fk = 0;
+    while (fk < limit) {
+      float bs = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        if (!((la >> u) & 1u)) continue;
+        if (have) {
+          const float bb[4] = {lb[u].x, lb[u].y, lb[u].z, lb[u].w};
+          if (!(iou_cxcywh(fb, bb) <= thr)) { la &= ~(1u << u); continue; }
+        }
+        if (better(ls[u], li[u], bs, bi)) { bs = ls[u]; bi = li[u]; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float s2 = __shfl_xor(bs, o, 64);
+        const int i2 = __shfl_xor(bi, o, 64);
+        if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+      }
+      if (lane == 0) { ws[wave] = bs; wi[wave] = bi; }
+      __syncthreads();
+      if (tid == 0) {
+        float sb = ws[0];
+        int b = wi[0];
+        for (int w = 1; w < 16; ++w)
+          if (better(ws[w], wi[w], sb, b)) { sb = ws[w]; b = wi[w]; }
+        best_s = b;
+      }
+      __syncthreads();
+      const int b = best_s;
+      if (b == 0x7fffffff) break;
+      if (tid == 0) keep[(size_t)set * max_keep + fk] = b;
+      ++fk;
+#pragma unroll
+      for (int u = 0; u < PER; ++u)
+        if (li[u] == b) la &= ~(1u << u);
+      const float4 v = *reinterpret_cast<const float4*>(bx + (size_t)b * 4);
+      fb[0] = v.x; fb[1] = v.y; fb[2] = v.z; fb[3] = v.w;
+      have = true;
+    }
+    if (fk >= limit || covered) {
+      kept = fk;
+      goto done;
+    }
+  }
+  {
   float kb[4] = {0.f, 0.f, 0.f, 0.f};
   bool have_kb = false;
   while (kept < limit) {
     float bs = -INFINITY;
     int bi = 0x7fffffff;
-    // groups of 8 slots: the group's box loads are all issued before its IoUs
+    // groups of 4 slots: the group's box loads are all issued before its IoUs
 #pragma unroll
-    for (int k0 = 0; k0 < kNmsRegSlots; k0 += 8) {
-      if (!((alive >> k0) & 0xffu)) continue;
-      float4 v[8];
+    for (int k0 = 0; k0 < kNmsRegSlots; k0 += 4) {
+      if (!((alive >> k0) & 0xfu)) continue;
+      float4 v[4];
       if (have_kb) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 4; ++u)
           if ((alive >> (k0 + u)) & 1u) v[u] = *reinterpret_cast<const float4*>(bx + (size_t)(tid + (k0 + u) * 1024) * 4);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int k = k0 + u;
         if (!((alive >> k) & 1u)) continue;
         const int i = tid + k * 1024;
@@ -195,6 +376,8 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
     kb[0] = v.x; kb[1] = v.y; kb[2] = v.z; kb[3] = v.w;
     have_kb = true;
   }
+  }
+done:
   if (tid == 0) n_keep[set] = kept;
   if (out_boxes) {   // kept boxes, zero padded to max_keep (zero boxes are skipped downstream)
     __syncthreads();

@@ -272,6 +272,39 @@ def test_nms_gpu_vs_golden(golden_dir):
         i += 1
 
 
+def test_nms_prefix_paths():
+    """nms_reg_kernel's prefix fast path (the top ~1024 candidates by score)
+    and its two ways out: a prefix that runs dry before max_output (a dense
+    cluster of 2,000 overlapping boxes on top: fallback to the full pass),
+    ties at the prefix threshold beyond the list (3,000 equal scores), and
+    max_output = 0 (keep everything).  Oracle: the reference's greedy NMS
+    restated (oracle.kpd_oracle.nms); tied scores may keep a different index
+    of equal score (torch's CPU sort is unstable), so those cases compare the
+    kept scores and boxes."""
+    from dll import _native
+    g = torch.Generator().manual_seed(7)
+    n = 5000
+    boxes = torch.rand(n, 4, generator=g) * torch.tensor([1.0, 1.0, 0.2, 0.2]) + torch.tensor([0.0, 0.0, 0.02, 0.02])
+    scores = torch.randperm(n, generator=g).float() / n * 0.5 + 0.3       # distinct scores
+    cl = torch.arange(2000)
+    boxes[cl] = torch.tensor([0.5, 0.5, 0.3, 0.3]) + 1e-3 * torch.rand(2000, 4, generator=g)
+    scores[cl] = 0.9 + 0.05 * torch.arange(2000, 0, -1).float() / 2000   # the cluster ranks first
+    for mo, thr in ((5, 0.3), (40, 0.3), (0, 0.5)):
+        got = _native.nms(boxes.to(DEV), scores.to(DEV), thr, mo).cpu()
+        ref = O.nms(boxes, scores, thr, mo if mo > 0 else None)
+        assert torch.equal(got, ref), (mo, thr)
+    tied = scores.clone()
+    tied[2000:2500] = 0.8 + 0.1 * torch.arange(500, 0, -1).float() / 500   # 500 distinct on top
+    tied[2500:5000] = 0.75                                                # then 2,500 ties
+    tied[cl] = 0.2 + 0.05 * torch.arange(2000, 0, -1).float() / 2000     # the cluster last
+    got = _native.nms(boxes.to(DEV), tied.to(DEV), 0.3, 5).cpu()           # kept within the 500
+    assert torch.equal(got, O.nms(boxes, tied, 0.3, 5))
+    got = _native.nms(boxes.to(DEV), tied.to(DEV), 0.3, 600).cpu()         # runs into the ties
+    ref = O.nms(boxes, tied, 0.3, 600)
+    assert got.numel() == ref.numel()
+    assert torch.equal(tied[got], tied[ref])
+
+
 def _dual_model(precision="fp32"):
     from dll.configs import KeypointHeadConfig, ModelConfig, TrainingConfig
     from dll.models import MultiPersonKeypointModel
