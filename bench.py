@@ -381,8 +381,9 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None, tag=None):
             kern[s] = (f, PEAK_TFLOPS["fp32"], f, "conv_mfma_kernel", f"{s} conv3x3 on v_mfma_f32_16x16x4_f32")
     if precision == "split":
         kern["hm_conv2"] += ("one stage = two launches: complete rounds of 224-row tiles "
-                             "(hmconv_kernel<256, 2, 0, 224, true, 256>) + the remaining rows as 192-row tiles "
-                             "(hmconv_kernel<256, 2, 0, 192, true, 256>); their rocprofv3 averages sum to avg_ms",)
+                             "(hmconv_kernel<256, 2, 0, 224, true, 256>) + the remaining rows as 160-row tiles "
+                             "(hmconv_kernel<256, 2, 0, 160, true, 256>; 192-row when 160 would need a second "
+                             "round); their rocprofv3 averages sum to avg_ms",)
     if precision in ("split", "mixed"):
         kern["hm_conv3"] += ("one stage = two launches: complete rounds of 256-row tiles + the remaining rows as "
                              "128-row tiles; their rocprofv3 averages sum to avg_ms",)

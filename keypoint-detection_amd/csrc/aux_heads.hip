@@ -225,8 +225,8 @@ __global__ __launch_bounds__(256) void kh_att_kernel(float* __restrict__ x, cons
 
 // Split-operand variant (KEYPOINT_HEAD on hmconv_kernel, MODE 2): the same
 // x * att (fp32), scaled by ROI r's power of two and written as f16 hi + lo in
-// [hi32 | lo32] groups at the padded position (y + 1, x + 1) of the ROI's 58x58
-// map (the zero border is never written).  |x * att| <= |x| <= bound: the
+// [hi32 | lo32] groups at the pixel's position of the hmconv layout (kHmPitch;
+// the zero borders are never written).  |x * att| <= |x| <= bound: the
 // scale 2^a, a = split_exp_of(bound), keeps hi below 2^15; the first conv's
 // input unscale reads the same bound from hsc[r][2].
 __global__ __launch_bounds__(256) void kh_att_split_kernel(const float* __restrict__ x, const float* __restrict__ sa1,
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void kh_att_split_kernel(const float* __restri
   if (rem == 0) hsc[(size_t)r * 4 + 2] = bnd;
   const float sc = ldexpf(1.f, split_exp_of(bnd));
   const float4* xp = reinterpret_cast<const float4*>(x + pix * 128);
-  _Float16* o = out + (((size_t)r * (G + 2) + yy + 1) * (G + 2) + xx + 1) * 256;
+  _Float16* o = out + hm_pos(r, yy, xx) * 256;
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #pragma unroll
   for (int q8 = 0; q8 < 16; ++q8) {   // 8 channels per step: one 16-byte hi and lo store each
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256) void kh_att2_kernel(const float* __restrict__ 
         hi[e] = (_Float16)e4[e];
         lo[e] = (_Float16)(e4[e] - (float)hi[e]);
       }
-      _Float16* o = out + (((size_t)r * (G + 2) + yy + 1) * (G + 2) + xx + 1) * 256 + (c4 / 32) * 64 + c4 % 32;
+      _Float16* o = out + hm_pos(r, yy, xx) * 256 + (c4 / 32) * 64 + c4 % 32;
       *reinterpret_cast<f16x4*>(o) = hi;
       *reinterpret_cast<f16x4*>(o + 32) = lo;
     }

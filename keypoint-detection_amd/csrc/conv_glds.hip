@@ -1056,22 +1056,25 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
 // ---------------------------------------------------------------- HeatmapHead convs, padded ROI maps
 // 3x3 conv + folded BN + ReLU on the 56x56 ROI maps of HeatmapHead
 // (heatmap_head.py:31-45,55-66), bf16 operands, fp32 accumulation.  The
-// activations are stored with a one-pixel zero border, [R][58][58][C], so a
-// tap (dy, dx) of output position m is input position m + 58 dy + dx with the
-// zero padding already in memory.  A GEMM row is a padded position; a tile is
+// activations are stored in the hmconv layout (kpd_kernels.h: rows of 57
+// positions, one zero column and one zero row shared between neighbours), so
+// a tap (dy, dx) of output position m is input position m + 57 dy + dx with
+// the zero padding already in memory.  A GEMM row is a position; a tile is
 // 256 consecutive positions, and its A operand for ALL nine taps of a
 // 64-channel chunk is one window of 384 positions (m0 - 64 .. m0 + 319) staged
 // once per chunk -- the per-tap A staging of the generic kernel (9 x 256 rows)
 // becomes 384 rows, so the LDS-DMA bytes per MFMA drop 1.7x (BN 256) to 3x
 // (BN 64): the generic kernel is bound by the ~70 GB/s per CU an L2 -> LDS
-// DMA stream sustains (tools/conv16_probe.py ablations).  The border rows and
-// columns of the GEMM are computed and discarded (the tile range starts at
-// padded row 1 of ROI 0; ~7 % extra MFMA work); outputs are stored to the
-// interior only, so the zero border written once at workspace creation stays.
+// DMA stream sustains (tools/conv16_probe.py ablations).  The border row and
+// column positions of the GEMM are computed and discarded (the tile range
+// starts at row 1 of ROI 0; 113 of 3249 positions per ROI, 3.5 % extra MFMA
+// work; a 58 x 58 frame had 6.8 %); outputs are stored to the interior only,
+// so the zero borders written once at workspace creation stay.
 //   BN 256: bf16 output (conv 1, 2), LDS-staged epilogue.
 //   BN 64 : conv 3 with the final 1x1 64->17 + sigmoid fused (mixed mode),
 //           written to the [B][P][17][56][56] heatmap at the ROI's slot.
-constexpr int HP = 58, HPP = HP * HP;   // padded ROI side, positions per ROI
+constexpr int HP = kHmPitch, HPP = kHmRoiPos;   // row pitch, positions per ROI (kpd_kernels.h)
+constexpr int HMS = 56;                          // ROI side
 constexpr int AWIN = 384;               // A window rows per chunk (tiles of <= 256 rows)
 // A window rows of a BMH-row tile: 64 halo rows above, >= 64 below (a tap
 // reads rows 64 - 59 .. 64 + 59 + BMH - 1 of the window)
@@ -1163,8 +1166,8 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   // a group with fewer live columns pairs with a full one on every SIMD)
   const int wm = EMODE == 2 ? wave % WAVES_M : wave / WAVES_N, wn = EMODE == 2 ? wave / WAVES_M : wave % WAVES_N;
   const int NTL = p.cout / BN;
-  const int m0 = HP + m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // padded positions [HP, R*HPP - HP)
-  if (m0 >= p.R * HPP - HP) return;   // (a padding tile of hmconv_mixed_kernel's tail)
+  const int m0 = HP + m_off + (L / NTL) * BMH, n0 = (L % NTL) * BN;   // GEMM rows: positions [HP, R*HPP)
+  if (m0 >= p.R * HPP) return;   // (a padding tile of hmconv_mixed_kernel's tail)
   // a K-step reads one 128-byte row piece: 64 bf16 channels, or (SPLIT) 32
   // channels as [hi32 | lo32] f16
   const int Mtot = p.R * HPP, cin = CIN ? CIN : p.cin, RB = SPLIT ? cin * 4 : cin * 2, NC = RB / 128, KT = NTAP * NC;
@@ -1574,8 +1577,8 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     r = m / HPP;
     const int rem = m - r * HPP;
     yy = rem / HP - 1;
-    xx = rem - (yy + 1) * HP - 1;
-    return m < Mtot - HP && yy >= 0 && yy < HP - 2 && xx >= 0 && xx < HP - 2;
+    xx = rem - (yy + 1) * HP;
+    return m < Mtot && yy >= 0 && xx < HMS;
   };
   if constexpr (PST) {
     // four parts of 112 rows x 128 columns staged through A1 + B1; every
@@ -1763,7 +1766,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
       if (!interior(m, rl, yy, xx)) continue;
       const int r = p.r0 + rl, sl = p.slot[r], bimg = r / p.P;
       const int pos = sl >= 0 ? sl : slot_pos(sl);
-      float* dst = p.heat + ((size_t)(bimg * p.P + pos) * NKF) * ((HP - 2) * (HP - 2)) + yy * (HP - 2) + xx;
+      float* dst = p.heat + ((size_t)(bimg * p.P + pos) * NKF) * (HMS * HMS) + yy * HMS + xx;
 #pragma unroll
       for (int s4 = 0; s4 < (NKF + 3) / 4; ++s4) {
         const int k = s4 * 4 + q4;
@@ -1771,7 +1774,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
         if (s4 * 4 + 1 < NKF && q4 == 1) val = o[i][s4 * 4 + 1];
         if (s4 * 4 + 2 < NKF && q4 == 2) val = o[i][s4 * 4 + 2];
         if (s4 * 4 + 3 < NKF && q4 == 3) val = o[i][s4 * 4 + 3];
-        if (k < NKF) dst[(size_t)k * ((HP - 2) * (HP - 2))] = sl >= 0 ? sigmoid_rcp(val + fw[NKF * 64 + k]) : 0.f;
+        if (k < NKF) dst[(size_t)k * (HMS * HMS)] = sl >= 0 ? sigmoid_rcp(val + fw[NKF * 64 + k]) : 0.f;
       }
     }
   } else {
@@ -1829,7 +1832,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
           *reinterpret_cast<f16x4*>(ob) = hi;
           *reinterpret_cast<f16x4*>(ob + 64) = lo;
         } else {
-          *reinterpret_cast<float4*>(p.outf + ((size_t)r * (HP - 2) * (HP - 2) + yy * (HP - 2) + xx) * p.nf +
+          *reinterpret_cast<float4*>(p.outf + ((size_t)r * HMS * HMS + yy * HMS + xx) * p.nf +
                                      (co - p.ns)) = make_float4(o[0], o[1], o[2], o[3]);
         }
       }
@@ -2012,9 +2015,9 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
     a.r0 = a0.r0 + r0;
     a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
     if (a0.out) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.ns * 4;
-    if (a0.outf) a.outf = a0.outf + (size_t)r0 * (HP - 2) * (HP - 2) * a.nf;
+    if (a0.outf) a.outf = a0.outf + (size_t)r0 * HMS * HMS * a.nf;
     a.in_bytes = (int)std::min<long>((long)nr * roi_bytes, kMaxDesc);   // (unused: per-tile descriptors)
-    const long rows = (long)nr * HPP - 2 * HP;
+    const long rows = (long)nr * HPP - HP;
     const dim3 grid((unsigned)((rows + BM - 1) / BM));
     // two taps per K-step (three for the 32-channel conv): one barrier per
     // 2-3 taps of MFMAs -- these convs have 96 / 32 / 16 live output columns,
@@ -2061,7 +2064,7 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
     a.in = static_cast<const char*>(a0.in) + (size_t)r0 * roi_bytes;
     if (!fin) a.out = static_cast<char*>(a0.out) + (size_t)r0 * HPP * a.cout * es;
     a.in_bytes = (int)std::min<long>((long)nr * roi_bytes, kMaxDesc);   // (unused: per-tile descriptors)
-    const long rows = (long)nr * HPP - 2 * HP;
+    const long rows = (long)nr * HPP - HP;
     // BN 256 with a 2-stage weight ring measured faster than BN 128 with 4
     // stages for conv 1 / 2 (89 / 233 us vs 92 / 256 us at 64 ROIs): the
     // wider tile halves the weight bytes per MFMA; conv 3 has 64 outputs
@@ -2177,13 +2180,19 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
       }
     }
 #endif
+    // tail tiles of conv 1 / conv 2: 160 rows when those fit one round (the
+    // last round then runs 160-row instead of 192-row tiles), else 192
+    const long F12 = rows / 224 / ncu * ncu, rem12 = rows - F12 * 224;
+    const bool t160 = (rem12 + 159) / 160 <= ncu;
+    const long H12 = t160 ? (rem12 + 159) / 160 : (rem12 + 191) / 192;
     if (split && !fin && bn == 256 && bm == 224 && (a.cin == 64 || a.cin == 256) && !dbg && !a.stamps) {
-      const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
-      if (mix_ok(F, H)) {   // conv 1 / conv 2
+      if (mix_ok(F12, H12)) {   // conv 1 / conv 2
         HmConvArgs m = a;
         dim3 g;
-        mix_set(m, F, H, g);
-        if (a.cin == 64) hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 192, 64, 1, false, -1>), g, dim3(NT), 0, st, m);
+        mix_set(m, F12, H12, g);
+        if (a.cin == 64 && t160) hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 160, 64, 1, false, -1>), g, dim3(NT), 0, st, m);
+        else if (a.cin == 64) hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 192, 64, 1, false, -1>), g, dim3(NT), 0, st, m);
+        else if (t160) hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 160, 256, 1, false, -1>), g, dim3(NT), 0, st, m);
         else hipLaunchKernelGGL((hmconv_mixed_kernel<256, 2, 224, 192, 256, 1, false, -1>), g, dim3(NT), 0, st, m);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -2191,13 +2200,13 @@ hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
       }
     }
     if (split && !fin && bn == 256 && bm == 224 && a.cin == 256 && !dbg && !no_tail12 && !a.stamps) {
-      const long F = rows / 224 / ncu * ncu, rem = rows - F * 224, H = (rem + 191) / 192;
-      if (F > 0 && rem > 0 && H <= ncu) {
-        const dim3 g1((unsigned)F), g2((unsigned)H);
+      if (F12 > 0 && rem12 > 0 && H12 <= ncu) {
+        const dim3 g1((unsigned)F12), g2((unsigned)H12);
         HmConvArgs a2 = a;
-        a2.m_off = (int)(F * 224);
+        a2.m_off = (int)(F12 * 224);
         hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 256>), g1, dim3(NT), 0, st, a);
-        hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 192, true, 256>), g2, dim3(NT), 0, st, a2);
+        if (t160) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 160, true, 256>), g2, dim3(NT), 0, st, a2);
+        else hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 192, true, 256>), g2, dim3(NT), 0, st, a2);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         continue;

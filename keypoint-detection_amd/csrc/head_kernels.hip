@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
 //   roi / roi_stats: the top-k channels (lane <- channel topk[b][lane] by a
 //     cross-lane read), as roi_align_kernel<1> writes them;
 //   out: x * att * 2^a as the split [hi32 | lo32] operand of the first
-//     KEYPOINT_HEAD conv, interior of the zero-bordered [R][58][58][128] map
+//     KEYPOINT_HEAD conv, interior of the zero-bordered [R][57 x 57][128] map
 //     (a = split_exp_of(bound of the image), hsc[r][2] = that bound), staged
 //     in LDS and stored as whole 28 KB rows;
 // replacing roi_align_kernel<1>, roi_align_kernel<2> (whose 128-channel fp32
@@ -536,8 +536,8 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
     }
   }
   __syncthreads();
-  // pixels 1..56 of padded row ph + 1 are one contiguous 28 KB run
-  uint4* dst = reinterpret_cast<uint4*>(out + (((size_t)r * (HM + 2) + ph + 1) * (HM + 2) + 1) * 256);
+  // the 56 pixels of row ph are one contiguous 28 KB run of the hmconv layout
+  uint4* dst = reinterpret_cast<uint4*>(out + hm_pos(r, ph, 0) * 256);
   const uint4* srcs = reinterpret_cast<const uint4*>(img);
 #pragma unroll
   for (int k = 0; k < HM * 512 / 16 / 256; ++k) dst[tid + 256 * k] = srcs[tid + 256 * k];
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(64) void hm_spool_kernel(const float* __restrict__ 
 // pixel (lane x < 56, LDS), then xs = (roi * cw) * sw with lane (p, c) on
 // channels 4c .. 4c+3 of pixel 4i + p (1 KiB contiguous per load, the roi row
 // loads issued first), stored as the first heatmap conv's operand: bf16
-// zero-bordered [R][58][58][64] (out_bf16 == 2), bf16 [R][3136][64] (1),
+// zero-bordered [R][57 x 57][64] (out_bf16 == 2), bf16 [R][3136][64] (1),
 // f32 (0), or (3) zero-bordered f16 hi | lo of xs * 2^a0(r), 32-channel
 // [hi32 | lo32] groups, a0 = split_exp_of(hsc[r][0]) (split heatmap convs).
 __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__ roi, const float* __restrict__ cw,
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
     const float sw = ssw[px];
     const float4 o = make_float4((v[i].x * cq.x) * sw, (v[i].y * cq.y) * sw, (v[i].z * cq.z) * sw, (v[i].w * cq.w) * sw);
     if (out_bf16 == 3) {
-      const size_t opix = ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1;
+      const size_t opix = hm_pos(r, y, px);
       const float ov[4] = {o.x * ssc, o.y * ssc, o.z * ssc, o.w * ssc};
       f16x4 hi, lo;
 #pragma unroll
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(64) void hm_sapply_kernel(const float* __restrict__
       *reinterpret_cast<f16x4*>(ob) = hi;
       *reinterpret_cast<f16x4*>(ob + 32) = lo;
     } else if (out_bf16) {
-      const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1
+      const size_t opix = out_bf16 == 2 ? hm_pos(r, y, px)
                                         : ((size_t)r * HM + y) * HM + px;
       bf16x4 ob;
       ob[0] = (__bf16)o.x; ob[1] = (__bf16)o.y; ob[2] = (__bf16)o.z; ob[3] = (__bf16)o.w;
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(512) void hm_attn_kernel(const float* __restrict__ 
       const float sw = ssw[j][px];
       const float4 o = make_float4((v[i].x * cq.x) * sw, (v[i].y * cq.y) * sw, (v[i].z * cq.z) * sw, (v[i].w * cq.w) * sw);
       if (out_bf16 == 3) {
-        const size_t opix = ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1;
+        const size_t opix = hm_pos(r, y, px);
         const float ov[4] = {o.x * ssc, o.y * ssc, o.z * ssc, o.w * ssc};
         f16x4 hi, lo;
 #pragma unroll
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(512) void hm_attn_kernel(const float* __restrict__ 
         *reinterpret_cast<f16x4*>(ob) = hi;
         *reinterpret_cast<f16x4*>(ob + 32) = lo;
       } else if (out_bf16) {
-        const size_t opix = out_bf16 == 2 ? ((size_t)r * (HM + 2) + y + 1) * (HM + 2) + px + 1
+        const size_t opix = out_bf16 == 2 ? hm_pos(r, y, px)
                                           : ((size_t)r * HM + y) * HM + px;
         bf16x4 ob;
         ob[0] = (__bf16)o.x; ob[1] = (__bf16)o.y; ob[2] = (__bf16)o.z; ob[3] = (__bf16)o.w;

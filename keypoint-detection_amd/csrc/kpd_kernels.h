@@ -55,15 +55,15 @@ struct Conv16Args {
 };
 hipError_t launch_conv16(const Conv16Args& a, int split, int out_bf16, hipStream_t st);
 
-// HeatmapHead 3x3 conv on zero-bordered ROI maps [R][58][58][C] bf16
+// HeatmapHead 3x3 conv on zero-bordered ROI maps [R][57 x 57][C] bf16
 // (conv_glds.hip, hmconv_kernel).  fin_w == null: bf16 output in the same
 // padded layout (interior only); else cout == 64 and the final 1x1 + sigmoid
 // is fused, writing heat [B][P][17][56][56] at the ROI's slot.
 struct HmConvArgs {
-  const void* in;        // [R][58][58][cin] bf16, or (split) f16 [hi32 | lo32] per 32 channels
+  const void* in;        // [R][57 x 57][cin] bf16, or (split) f16 [hi32 | lo32] per 32 channels
   const void* wt;        // [cout][9][cin] bf16 (BN folded), or (split) f16 [hi32 | lo32] scaled 2^w_exp
   const float* bias;     // [cout]
-  void* out;             // [R][58][58][cout] bf16, or (split) f16 [hi32 | lo32]
+  void* out;             // [R][57 x 57][cout] bf16, or (split) f16 [hi32 | lo32]
   int R, cin, cout;
   // split (fp32-accurate) mode: per-ROI bounds hsc[r][4]; the operand scale of
   // ROI r is 2^a with a = split_exp_of(c + s * hsc[r][idx]) (kpd_common.h)
@@ -89,13 +89,25 @@ struct HmConvArgs {
   // ntap = 10 when the ResidualBlock's 1x1 downsample rides along as a tenth
   // tap; per column co: v = relu6(acc + bias), v = relu6(v * kh_ps + kh_pt),
   // (ntap 10) v = relu6(v + downsample + kh_bd); columns [0, ns) -> out (split,
-  // [R][58][58][ns]), [ns, ns + nf) -> outf fp32 [R][56][56][nf]
+  // [R][57 x 57][ns]), [ns, ns + nf) -> outf fp32 [R][56][56][nf]
   const float *kh_ps, *kh_pt, *kh_bd;
   float* outf;
   int ns, nf, ntap;
 };
 hipError_t launch_hmconv(const HmConvArgs& a, hipStream_t st);
-constexpr int kHmPad = 58;   // padded ROI side of the hmconv layout
+// The hmconv layout of the per-ROI activation maps (HeatmapHead and
+// KEYPOINT_HEAD convs): per ROI 57 rows of 57 positions, interior pixel
+// (y, x) at position r * kHmRoiPos + (y + 1) * kHmPitch + x.  Row 0 and
+// column 56 are zero: column 56 is the right border of its row and the left
+// border of the next row, row 0 the top border of its ROI and the bottom
+// border of the previous one; ROI 0's top-left neighbour (position -1) and
+// the last ROI's bottom border lie outside the tensor and read as zero (the
+// conv kernels' window loads are range-checked).  3249 positions per ROI
+// instead of a 58 x 58 frame's 3364: 3.4 % fewer GEMM rows in every conv.
+constexpr int kHmPitch = 57, kHmRoiPos = kHmPitch * kHmPitch;
+__host__ __device__ inline size_t hm_pos(size_t r, int y, int x) {
+  return r * kHmRoiPos + (size_t)(y + 1) * kHmPitch + x;
+}
 
 // FPN level 0 by linearity (split mode): conv3x3(L0(tap0) + up4(lat1)) =
 // conv3x3'(tap0) [composite weights W3.L0, 16 input channels]
@@ -259,7 +271,7 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
                           hipStream_t st);
 // Dual head, split precision: one 128-channel ROI align pass writing the top-k
 // HeatmapHead input (roi, roi_stats) and KEYPOINT_HEAD's attention-applied
-// split operand (out: [R][58][58][128] hi|lo f16 interior; hsc[r][2] = bound)
+// split operand (out: [R][57 x 57][128] hi|lo f16 interior; hsc[r][2] = bound)
 hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk, const float* boxes, int R, int P,
                         float* roi, float* roi_stats, const void* w1s, int w1_exp, const float* b1, const float* w2,
                         const float* b2, const float* bound, int bdiv, int bstride, float* hsc, void* out,
@@ -310,7 +322,7 @@ hipError_t launch_person_decode(const float* head, int B, int hc, const float* a
                                 float conf, float* cand_boxes, float* cand_scores, hipStream_t st);
 hipError_t launch_kh_att(float* x, const float* sa1, const float* w, const float* b, size_t npix, hipStream_t st);
 // the attention-weighted KEYPOINT_HEAD input as the split operand of the first
-// hmconv (KH mode): [R][58][58][128] f16 [hi32 | lo32], ROI r scaled by
+// hmconv (KH mode): [R][57 x 57][128] f16 [hi32 | lo32], ROI r scaled by
 // 2^split_exp_of(bound[(r / bdiv) * bstride]), which is also stored to hsc[r][2]
 // the same with the spatial attention's 1x1 128 -> 64 fused (split f16 MFMA;
 // w1s = pack_split_1x1 layout [64][4][hi32 | lo32] scaled 2^w1_exp)

@@ -151,7 +151,7 @@ struct Work {  // device workspace carve for one (B,H,W,nbox,P) shape
   // KEYPOINT_HEAD
   float *kx = nullptr, *ksa = nullptr, *kds1 = nullptr, *krb1 = nullptr, *kds2 = nullptr, *krb2 = nullptr;
   float *kr3 = nullptr, *kv1 = nullptr, *kpr = nullptr, *kpv = nullptr, *klr = nullptr, *klv = nullptr;
-  // KEYPOINT_HEAD on the split hmconv path: zero-bordered [R][58][58][C] f16
+  // KEYPOINT_HEAD on the split hmconv path: zero-bordered [R][57 x 57][C] f16
   // [hi32 | lo32] operands (x * att, ResidualBlock 1 / 2 outputs) and the
   // per-image FPN level-0 maximum (their scale bound, written by topk_kernel)
   void *kxs = nullptr, *kr1s = nullptr, *kr2s = nullptr;
@@ -692,8 +692,8 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
     w.cw = c.take<float>(R * 64);
     w.hsc = c.take<float>(R * 4);
     w.smap = c.take<float>(px * 2);
-    // mixed: zero-bordered 58x58 ROI maps for the padded heatmap convs (hmconv_kernel)
-    const size_t pxp = hm_padded(p) ? R * kHmPad * kHmPad : px;
+    // mixed: zero-bordered ROI maps (hmconv layout, kpd_kernels.h) for the padded heatmap convs (hmconv_kernel)
+    const size_t pxp = hm_padded(p) ? R * kHmRoiPos : px;
     w.xs = c.take<char>(pxp * 64 * es);
     w.h1 = c.take<char>(pxp * 256 * es);
     w.h2 = c.take<char>(pxp * 256 * es);
@@ -714,7 +714,7 @@ size_t carve(kpd_plan* p, const Dims& d, char* base, Work& w) {
       w.klr = c.take<float>(R * 256);
       w.klv = c.take<float>(R * 128);
       if (p->kh_split) {
-        const size_t pp = R * kHmPad * kHmPad;
+        const size_t pp = R * kHmRoiPos;
         w.kxs = c.take<char>(pp * 128 * 4);
         w.kr1s = c.take<char>(pp * (size_t)p->kh_s[0].ns * 4);
         w.kr2s = c.take<char>(pp * (size_t)p->kh_s[1].ns * 4);
@@ -1690,9 +1690,9 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
   if (int rc = mark(5)) return rc;
   if (debug) p->debug["roi"] = {w.roi, sizeof(float) * (size_t)R * 3136 * 64};
   if (int rc = run_heatmap_head(p, w, R, P, heat_out, st, KPD_HEAD_ALL, nullptr,
-                                 take_stamps("stamps_hm2", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
-                                 take_stamps("stamps_hm3", (size_t)(((long)R * 58 * 58 - 116 + 255) / 256) * 2),
-                                 take_stamps("stamps_hm1", (size_t)(((long)R * 58 * 58 - 116 + 255) / 224) * 2)))
+                                 take_stamps("stamps_hm2", (size_t)(((long)R * kHmRoiPos - kHmPitch + 255) / 224) * 2),
+                                 take_stamps("stamps_hm3", (size_t)(((long)R * kHmRoiPos - kHmPitch + 255) / 256) * 2),
+                                 take_stamps("stamps_hm1", (size_t)(((long)R * kHmRoiPos - kHmPitch + 255) / 224) * 2)))
     return rc;
   {
     Stage sg(p, "hm_final_decode", st);

@@ -40,8 +40,12 @@ def label(forward):
     for k in forward:
         targs = [t.strip() for t in k[len("hmconv_kernel<"):].split(">")[0].split(",")] \
             if k.startswith("hmconv_kernel<") else []
+        margs = [t.strip() for t in k[len("hmconv_mixed_kernel<"):].split(">")[0].split(",")] \
+            if k.startswith("hmconv_mixed_kernel<") else []
         if k.startswith("fpn0x_kernel"):
             out.append("fpn0")
+        elif margs:   # <BN, SB, BMH, BMT, CIN, ...>: full + tail tiles in one launch
+            out.append("hm_conv3" if margs[0] == "64" else "hm_conv1" if margs[4] == "64" else "hm_conv2")
         elif len(targs) >= 10 and targs[9] == "2":
             out.append("kh_conv")   # KEYPOINT_HEAD convs (MODE 2), dual-head configs
         elif k.startswith("hmconv_kernel<64"):
