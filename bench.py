@@ -357,7 +357,7 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None, tag=None):
         pd = (k - 1) // 2
         h1, w1 = (h1 + 2 * pd - k) // st + 1, (w1 + 2 * pd - k) // st + 1
     split_fpn = precision in ("split", "mixed") and hf == 4 * h1 and wf == 4 * w1
-    pad = 58 * 58 / (56 * 56)    # hmconv computes the padded ROI rows (border rows discarded)
+    pad = 57 * 57 / (56 * 56)    # hmconv computes every position of the 57x57 layout (borders discarded)
     kern = {}
     if split_fpn:
         ex = 3 * 2.0 * hf * wf * (5 * 32 * 128 + 36 * 128 * 128 / 16) * B
@@ -372,11 +372,11 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None, tag=None):
         f = fl[s] * B
         if precision == "split":
             kern[s] = (f, PEAK_TFLOPS["bf16"], 3 * f * pad, "hmconv_kernel<SPLIT>",
-                       f"{s} conv3x3 on zero-bordered ROI maps, fp32-accurate: 3 f16 products per MAC on "
+                       f"{s} conv3x3 on the zero-bordered hmconv layout, fp32-accurate: 3 f16 products per MAC on "
                        "v_mfma_f32_16x16x32_f16")
         elif precision == "mixed":
             kern[s] = (f, PEAK_TFLOPS["bf16"], f * pad, "hmconv_kernel",
-                       f"{s} conv3x3 on zero-bordered ROI maps, bf16 operands on v_mfma_f32_16x16x32_bf16")
+                       f"{s} conv3x3 on the zero-bordered hmconv layout, bf16 operands on v_mfma_f32_16x16x32_bf16")
         else:
             kern[s] = (f, PEAK_TFLOPS["fp32"], f, "conv_mfma_kernel", f"{s} conv3x3 on v_mfma_f32_16x16x4_f32")
     if precision == "split":
