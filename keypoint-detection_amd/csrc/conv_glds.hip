@@ -1107,10 +1107,14 @@ constexpr int hm_epi_parts() { return BMH > 256 ? 2 : 1; }
 // NTAP (MODE 2): 10 = the 3x3 taps plus the ResidualBlock's 1x1 downsample as
 // a tenth K-step per chunk (the centre tap's A rows, its own weights) into a
 // second accumulator set.
-template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE>
+// A-window buffers: 2 (chunk c + 1's window lands while chunk c's taps run),
+// 1 when the input is a single 128-byte chunk (CIN 32 split: one window per tile)
+template <int CIN, bool SPLIT>
+constexpr int hm_nab() { return (CIN > 0 && (SPLIT ? CIN * 4 : CIN * 2) == 128) ? 1 : 2; }
+template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE, int NAB = 2>
 constexpr int hmconv_lds_bytes() {
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
-  constexpr int RING = 2 * hm_awin<BMH>() * ROWB + SB * BN * ROWB * TPS;
+  constexpr int RING = NAB * hm_awin<BMH>() * ROWB + SB * BN * ROWB * TPS;
   constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
   return RING > EPI ? RING : EPI;
 }
@@ -1149,12 +1153,14 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   constexpr int ABUF = AW * ROWB, BSTAGE = BN * ROWB * TPS;
   static_assert(TPS == 1 || (SPLIT && NTAP % TPS == 0), "taps per step");
   constexpr bool FINAL = EMODE == 1;
-  static_assert(hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE>() <= 160 * 1024, "LDS budget");
+  constexpr int NAB = hm_nab<CIN, SPLIT>();
+  static_assert(hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE, NAB>() <= 160 * 1024, "LDS budget");
+  static_assert(!PST || NAB == 2, "persistent tiles: two window buffers");
   static_assert(!PST || (SPLIT && EMODE == 0 && SB == 2 && TPS == 1 && !DB && NW == 8 && NTAP == 9 && BN == 256 &&
                          BMH <= 224 && DBG == 0), "persistent tiles: split conv 1 / conv 2 (BN = cout = 256)");
   // window buffer of chunk c, weight stage s (PST: [A0 | B0 | A1 | B1])
-  auto a_at = [&](int c) { return PST ? (c & 1) * (ABUF + BSTAGE) : (c & 1) * ABUF; };
-  auto b_at = [&](int st) { return PST ? st * (ABUF + BSTAGE) + ABUF : 2 * ABUF + st * BSTAGE; };
+  auto a_at = [&](int c) { return PST ? (c & 1) * (ABUF + BSTAGE) : NAB == 1 ? 0 : (c & 1) * ABUF; };
+  auto b_at = [&](int st) { return PST ? st * (ABUF + BSTAGE) + ABUF : NAB * ABUF + st * BSTAGE; };
 
   int tid = threadIdx.x;
   // PST: per tile, tid is opaque, so that the lane-dependent offsets are
@@ -1848,7 +1854,8 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
 template <int BN, int SB, int DBG = 0, int BMH = BM, bool SPLIT = false, int CIN = 0, int TPS = 1, bool DB = false,
           int NW = 8, int MODE = -1, int NTAP = 9>
 __global__ __launch_bounds__(NW * 64) void hmconv_kernel(const HmConvArgs p) {
-  __shared__ __attribute__((aligned(1024))) char lds[hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE>()];
+  __shared__ __attribute__((aligned(1024))) char lds[hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE,
+                                                                      hm_nab<CIN, SPLIT>()>()];
   hmconv_tile<BN, SB, DBG, BMH, SPLIT, CIN, TPS, DB, NW, MODE, NTAP>(p, lds, xcd_remap(blockIdx.x, gridDim.x),
                                                                         p.m_off);
 }
@@ -2019,6 +2026,15 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
     a.in_bytes = (int)std::min<long>((long)nr * roi_bytes, kMaxDesc);   // (unused: per-tile descriptors)
     const long rows = (long)nr * HPP - HP;
     const dim3 grid((unsigned)((rows + BM - 1) / BM));
+    // the regression conv (cin 32: one input chunk, one window per tile)
+    // takes 512-row tiles: 64 x 64 per wave (0.83 fragment reads per MFMA
+    // instead of 1.0) and half the per-tile prologues / epilogues of its
+    // 3 K-steps
+    const dim3 grid512((unsigned)((rows + 511) / 512));
+    // ResidualBlock 2 (cin 64, 32 live columns): 384-row tiles, 48 x 64 per
+    // wave (a 512-row window pair + two weight stages fill the 160 KB)
+    const dim3 grid384((unsigned)((rows + 383) / 384));
+    static const bool kh_bm256 = kpd_diag_env("KPD_KH_BM256") != nullptr;   // A/B: 256-row tiles for both
     // two taps per K-step (three for the 32-channel conv): one barrier per
     // 2-3 taps of MFMAs -- these convs have 96 / 32 / 16 live output columns,
     // so a single tap's MFMAs are too few to amortise a barrier and the DMA
@@ -2028,10 +2044,14 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
       if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 3, 0, BM, true, 128, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
       else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 64, 1, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
       else hipLaunchKernelGGL((hmconv_kernel<64, 4, 0, BM, true, 32, 1, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
-    } else {
+    } else if (kh_bm256) {
       if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 2, 0, BM, true, 128, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
       else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 64, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
       else hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, BM, true, 32, 3, false, 8, 2, 9>), grid, dim3(NT), 0, st, a);
+    } else {
+      if (sel == 1) hipLaunchKernelGGL((hmconv_kernel<128, 2, 0, BM, true, 128, 2, false, 8, 2, 10>), grid, dim3(NT), 0, st, a);
+      else if (sel == 2) hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, 384, true, 64, 2, false, 8, 2, 10>), grid384, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((hmconv_kernel<64, 2, 0, 512, true, 32, 3, false, 8, 2, 9>), grid512, dim3(NT), 0, st, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
