@@ -115,6 +115,17 @@ __global__ __launch_bounds__(1024) void nms_kernel(const float* __restrict__ box
 // kept last) and finds the best survivor at the same time -- the same
 // keep-best / drop-IoU>thr sequence as nms_kernel (same IoU arithmetic and
 // tie-break), without its global alive array and two sweeps per kept box.
+// slot of this lane in a list that every wave appends to: one LDS atomic per
+// wave (the lanes with `in` set take consecutive slots in lane order)
+__device__ __forceinline__ int wave_append(bool in, int* counter, int lane) {
+  const unsigned long long m = __ballot(in);
+  if (!m) return 0;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (int)__popcll(m & ((1ull << lane) - 1ull));
+}
 constexpr int kNmsRegSlots = 32;
 constexpr int kNmsPrefix = 1024;   // target size of the fast path's prefix S
 constexpr int kNmsList = 2048;     // LDS list capacity for S (ties at its threshold included)
@@ -226,12 +237,11 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
     for (int pass = 0; pass < 2; ++pass) {   // pass 0: keys > tau, pass 1: keys == tau
 #pragma unroll
       for (int k = 0; k < kNmsRegSlots; ++k) {
-        if (!((alive >> k) & 1u)) continue;
         const unsigned key = key_of(s[k]);
-        const bool in = pass == 0 ? (tau == 0u || key > tau) : (tau != 0u && key == tau);
-        if (!in) continue;
-        const int pos = atomicAdd(&sh_cnt, 1);
-        if (pos < kNmsList) { l_idx[pos] = tid + k * 1024; l_sc[pos] = s[k]; }
+        const bool in = ((alive >> k) & 1u) &&
+                        (pass == 0 ? (tau == 0u || key > tau) : (tau != 0u && key == tau));
+        const int pos = wave_append(in, &sh_cnt, lane);
+        if (in && pos < kNmsList) { l_idx[pos] = tid + k * 1024; l_sc[pos] = s[k]; }
       }
       __syncthreads();
       if (pass == 0 && sh_cnt > kNmsList) break;   // (cannot happen: keys > tau number < kNmsPrefix)
@@ -244,11 +254,9 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < kNmsRegSlots; ++k) {
-        if (!((alive >> k) & 1u)) continue;
-        if (!(key_of(s[k]) > tau)) continue;
-        const int pos = atomicAdd(&sh_cnt, 1);
-        l_idx[pos] = tid + k * 1024;
-        l_sc[pos] = s[k];
+        const bool in = ((alive >> k) & 1u) && key_of(s[k]) > tau;
+        const int pos = wave_append(in, &sh_cnt, lane);
+        if (in) { l_idx[pos] = tid + k * 1024; l_sc[pos] = s[k]; }
       }
       __syncthreads();
       m = sh_cnt;
