@@ -69,6 +69,9 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
   float* l2 = l3 + P3 * LG;             // [P2][16]
   float* red = l2;                      // [NW][P3][16] lat3 partials (dead before l2 is written)
   float* mx = l2 + max(P2, NW * P3) * LG;   // [3][NW] per-wave tap maxima
+  // SPLIT: per-wave transpose scratch of one lateral-1 tile (16 pixels x
+  // [hi16 | lo16] halves, 1 KB), so that a lane stores 16 contiguous bytes
+  _Float16* tsc = reinterpret_cast<_Float16*>(mx + 4 * NW) + (threadIdx.x >> 6) * (16 * 2 * LG);
   // grid (B rounded up to 8, 8): workgroup id b + Bp * cg sits on XCD b % 8,
   // so an image's 8 channel groups share one L2 and its taps leave HBM once
   const int b = blockIdx.x, cg = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -203,6 +206,7 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
   // lat1 = L1 . tap1 + up(lat2) -> HBM (fp32, or split by the image's bound)
   float s_l = 1.f, s_f = 1.f;
   _Float16* outs = nullptr;
+  const int part = lane & 3;
   if constexpr (SPLIT) {
     float M1 = mx[0], M2 = mx[NW], M3 = mx[2 * NW];
 #pragma unroll
@@ -217,8 +221,9 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
     s_l = ldexpf(1.f, a_l);
     s_f = ldexpf(1.f, a_f);
     if (tid == 0) amax_publish_img(p.amax + (size_t)p.n * kAmaxStride, b, bound);
-    // hi|lo rows: pixel pp at halves [pp][2 * 128]; channel co in group co / 32: hi at +co % 32, lo 32 further
-    outs = p.lat1_split + (size_t)b * P1 * 256 + (co >> 5) * 64 + (co & 31);
+    // hi|lo rows: pixel pp at halves [pp][2 * 128]; channel co in group co / 32: hi at +co % 32, lo 32 further.
+    // A lane stores 8 halves: pixel lane / 4, part lane % 4 = (hi | lo) x (channels 0-7 | 8-15) of the group
+    outs = p.lat1_split + (size_t)b * P1 * 256 + (cg >> 1) * 64 + (cg & 1) * 16 + (part >> 1) * 32 + (part & 1) * 8;
   }
   {
     constexpr int JB = T1;
@@ -252,11 +257,18 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
           if constexpr (SPLIT) {
             const float xs = v * s_l;
             const _Float16 hi = (_Float16)xs;
-            outs[(size_t)pp * 256] = hi;
-            outs[(size_t)pp * 256 + 32] = (_Float16)(xs - (float)hi);
+            tsc[(4 * g + e) * 32 + r16] = hi;
+            tsc[(4 * g + e) * 32 + 16 + r16] = (_Float16)(xs - (float)hi);
           } else {
             out[(size_t)pp * 128] = v;
           }
+        }
+        if constexpr (SPLIT) {
+          // (LDS operations of one wave complete in order: the reads see
+          // every lane's writes, and the next tile's writes follow them)
+          const int q = lane >> 2, pp = t * 16 + q;
+          const uint4 v = *reinterpret_cast<const uint4*>(tsc + q * 32 + part * 8);
+          if (pp < P1) *reinterpret_cast<uint4*>(outs + (size_t)pp * 256) = v;
         }
       }
     }
@@ -306,12 +318,13 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
 
 size_t lateral_chain_lds_bytes(const LatChainArgs& a) {
   const size_t P2 = (size_t)a.h2 * a.w2, P3 = (size_t)a.h3 * a.w3;
-  return (P3 * LG + std::max(P2, NW * P3) * LG + 3 * NW) * sizeof(float);
+  // (+ the split path's per-wave transpose tiles: 16 x 32 halves per wave)
+  return (P3 * LG + std::max(P2, NW * P3) * LG + 4 * NW) * sizeof(float) + (size_t)NW * 16 * 2 * LG * 2;
 }
 
 bool lateral_chain_ok(const LatChainArgs& a) {
   return a.c1 == 32 && a.c2 == 48 && a.c3 == 576 && a.h1 > 0 && a.w1 > 0 && a.h2 > 0 && a.w2 > 0 && a.h3 > 0 &&
-         a.w3 > 0 && a.h3 * a.w3 <= 16 * 8 && lateral_chain_lds_bytes(a) <= 64 * 1024 &&
+         a.w3 > 0 && a.h3 * a.w3 <= 16 * 8 && lateral_chain_lds_bytes(a) <= 80 * 1024 &&
          (!a.lat1_split || a.amax);
 }
 
