@@ -385,23 +385,45 @@ __global__ __launch_bounds__(256) void kh_pool_kernel(const float* __restrict__ 
   const int r = blockIdx.x, nq = C / 4, rpc = (G + o - 1) / o + 1;   // rows per cell (upper bound)
   const float* src = in + (size_t)r * GP * C;
   const int items = o * o * rpc * nq;
-  for (int t = threadIdx.x; t < items; t += blockDim.x) {
-    const int q = t % nq, rest = t / nq, dy = rest % rpc, cell = rest / rpc, i = cell / o, j = cell - i * o;
-    const int y0 = (i * G) / o, y1 = ((i + 1) * G + o - 1) / o;
-    const int x0 = (j * G) / o, x1 = ((j + 1) * G + o - 1) / o;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int y = y0 + dy;
-    if (y < y1)
-      for (int xb = x0; xb < x1; xb += 8) {   // 8 loads in flight, summed in x order as before
-        float4 v[8];
+  // IU items per thread at a time, XB columns of each: IU * XB loads in
+  // flight per batch (one memory round trip), each item still summed in x
+  // order
+  constexpr int IU = 4, XB = 2;
+  for (int t0 = threadIdx.x; t0 < items; t0 += IU * blockDim.x) {
+    const float* rowp[IU];
+    int len[IU], dst[IU], lmax = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (xb + u < x1) v[u] = *reinterpret_cast<const float4*>(src + ((size_t)y * G + xb + u) * C + q * 4);
+    for (int k = 0; k < IU; ++k) {
+      const int t = t0 + k * blockDim.x;
+      const int tt = min(t, items - 1);
+      const int q = tt % nq, rest = tt / nq, dy = rest % rpc, cell = rest / rpc, i = cell / o, j = cell - i * o;
+      const int y0 = (i * G) / o, y1 = ((i + 1) * G + o - 1) / o;
+      const int x0 = (j * G) / o, x1 = ((j + 1) * G + o - 1) / o;
+      const int y = y0 + dy;
+      len[k] = t < items && y < y1 ? x1 - x0 : 0;
+      rowp[k] = src + ((size_t)min(y, G - 1) * G + x0) * C + q * 4;
+      dst[k] = t < items ? (cell * rpc + dy) * C + q * 4 : -1;
+      lmax = max(lmax, len[k]);
+    }
+    float4 s[IU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (xb + u < x1) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
-      }
-    *reinterpret_cast<float4*>(part + ((size_t)cell * rpc + dy) * C + q * 4) = s;
+    for (int k = 0; k < IU; ++k) s[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int xb = 0; xb < lmax; xb += XB) {
+      float4 v[IU][XB];
+#pragma unroll
+      for (int k = 0; k < IU; ++k)
+#pragma unroll
+        for (int u = 0; u < XB; ++u)
+          if (xb + u < len[k]) v[k][u] = *reinterpret_cast<const float4*>(rowp[k] + (size_t)(xb + u) * C);
+#pragma unroll
+      for (int k = 0; k < IU; ++k)
+#pragma unroll
+        for (int u = 0; u < XB; ++u)
+          if (xb + u < len[k]) { s[k].x += v[k][u].x; s[k].y += v[k][u].y; s[k].z += v[k][u].z; s[k].w += v[k][u].w; }
+    }
+#pragma unroll
+    for (int k = 0; k < IU; ++k)
+      if (dst[k] >= 0) *reinterpret_cast<float4*>(part + dst[k]) = s[k];
   }
   __syncthreads();
   const int n = C * o * o;
