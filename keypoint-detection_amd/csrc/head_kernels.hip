@@ -554,9 +554,21 @@ __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__
   const int r = blockIdx.x, c = threadIdx.x;
   const float* st = roi_stats + (size_t)r * HM * 2 * TOPK;
   float s = 0.f, m = -INFINITY;
-  for (int row = 0; row < HM; ++row) {
-    s += st[row * 2 * TOPK + c];
-    m = fmaxf(m, st[row * 2 * TOPK + TOPK + c]);
+  // rows in batches of 14: 28 loads in flight, sums still in row order
+  constexpr int RB = 14;
+  static_assert(HM % RB == 0, "row batches");
+  for (int row0 = 0; row0 < HM; row0 += RB) {
+    float vs[RB], vm[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      vs[u] = st[(row0 + u) * 2 * TOPK + c];
+      vm[u] = st[(row0 + u) * 2 * TOPK + TOPK + c];
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s += vs[u];
+      m = fmaxf(m, vm[u]);
+    }
   }
   avg[c] = s / (float)HMP;
   mx[c] = m;
@@ -573,6 +585,7 @@ __global__ __launch_bounds__(64) void hm_chattn_kernel(const float* __restrict__
     const int j = c & 3;
     const float* v = (c < 4) ? avg : mx;
     float a = b0[j];
+#pragma unroll 16
     for (int k = 0; k < TOPK; ++k) a = fmaf(w0[j * TOPK + k], v[k], a);
     h[c] = fmaxf(a, 0.f);
   }
