@@ -135,11 +135,14 @@ def parse(argv=None):
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r04" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run (entries are "
                          "stamped with the hash of the kernel sources they were measured on)")
-    ap.add_argument("--c3", type=int, default=1,
-                    help="N=1: also run BASELINE C3 (B=256 256x192, person detector + NMS + heatmap head + "
-                         "KEYPOINT_HEAD) as the labelled 'configs.C3' object (0 = skip)")
-    ap.add_argument("--c3-only", action="store_true", help="run only the C3 object (profiling passes)")
-    ap.add_argument("--c3-cpu-sample", type=int, default=16, help="images in C3's CPU-baseline sample")
+    ap.add_argument("--configs", default="auto",
+                    help="labelled BASELINE config objects after the C2 headline: 'auto' = C3,C5 at N=1 and "
+                         "C4,C5 at N>1 (C4 = the C3 pipeline per rank with RCCL collation); a comma list; 'none'")
+    ap.add_argument("--only", default=None, choices=sorted(PIPELINES),
+                    help="run only this config object (profiling passes)")
+    ap.add_argument("--c3-only", dest="only", action="store_const", const="C3", help="= --only C3")
+    ap.add_argument("--cfg-batch", type=int, default=0, help="images per rank of the config objects (0 = theirs)")
+    ap.add_argument("--cfg-cpu-sample", type=int, default=8, help="images in the config objects' CPU-baseline sample")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="test mode: no GPU; gloo ranks on the CPU run a stand-in forward through the same "
                          "launcher, barrier, timing and collation code (tests/test_bench_launch.py)")
@@ -260,19 +263,37 @@ def launch_ranks(n, argv):
 class StandinModel:
     """--cpu-standin: a cheap deterministic forward with the drop-in's output
     contract ([n,P,1,17,2] keypoints, [n,P,1,17,3] one-hot visibilities,
-    [n,P,17,56,56] heatmaps), so the launcher / timing / collation code runs
-    without a GPU.  It is not the model and never produces a bench number."""
+    [n,P,17,56,56] heatmaps, the dual head's kh_* outputs; without boxes the
+    detector branch's P = max_persons, box list and box_scores), so the
+    launcher / timing / collation code runs without a GPU.  keypoints[..., 0]
+    carry (offset + local image index) / 1e4, so a collated copy shows where
+    every rank's slab landed.  It is not the model and never produces a bench
+    number."""
     num_keypoints = 17
 
+    def __init__(self, offset=0, max_persons=5):
+        self.offset, self.max_persons = offset, max_persons
+
     def __call__(self, batch):
-        img, boxes = batch["image"], batch["bboxes"]
-        n, p = boxes.shape[:2]
+        img = batch["image"] if isinstance(batch, dict) else batch
+        n = img.size(0)
+        if isinstance(batch, dict) and "bboxes" in batch:
+            boxes = batch["bboxes"]
+        else:
+            g = torch.Generator().manual_seed(self.offset)
+            boxes = torch.rand(n, self.max_persons, 4, generator=g)
+        p = boxes.size(1)
         m = img.mean(dim=(1, 2, 3))
-        k = (boxes[..., :2].unsqueeze(2) + 0.01 * m.view(n, 1, 1, 1)).expand(n, p, 17, 2).clamp(0, 1)
+        k = (boxes[..., :2].unsqueeze(2) + 0.01 * m.view(n, 1, 1, 1)).expand(n, p, 17, 2).clamp(0, 1).clone()
+        k[..., 0] = ((self.offset + torch.arange(n, dtype=torch.float32)) / 1e4).view(n, 1, 1)
         v = torch.zeros(n, p, 17, 3)
         v[..., 2] = 1.0
-        return {"keypoints": k.unsqueeze(2).contiguous(), "visibilities": v.unsqueeze(2),
-                "heatmap": torch.zeros(n, p, 17, 56, 56)}
+        out = {"keypoints": k.unsqueeze(2).contiguous(), "visibilities": v.unsqueeze(2),
+               "heatmap": torch.zeros(n, p, 17, 56, 56), "kh_keypoints": k.unsqueeze(2) * 0.5,
+               "kh_visibilities": v.unsqueeze(2) * 0.5, "boxes": [boxes[i] for i in range(n)]}
+        if not (isinstance(batch, dict) and "bboxes" in batch):
+            out["box_scores"] = boxes[..., 0].clone()
+        return out
 
 
 def main_standin(a, world, rank, dist):
@@ -308,6 +329,11 @@ def main_standin(a, world, rank, dist):
         line["collated_ok"] = bool(all(
             torch.equal(coll["visibilities"][s:e, :, 0, :, 2], torch.ones(e - s, P, 17))
             for s, e in (shard_range(B * world, world, r) for r in range(world))))
+    cfgs = {}
+    for name in config_names(a, world):
+        cfgs[name] = run_pipeline(name, a, torch.device("cpu"), None, world, rank, dist, cpu=False, standin=True)
+    if cfgs:
+        line["configs"] = cfgs
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
@@ -421,70 +447,155 @@ def roofline(precision, stages, fl, B, H, W, pmc, dom=None, tag=None):
     return r
 
 
-C3 = dict(B=256, H=256, W=192, max_persons=5)
+# BASELINE.json configs beyond the C2 headline, as labelled objects of the
+# line (per-rank batch: B images on every rank, global B x N)
+PIPELINES = {
+    "C3": dict(B=256, H=256, W=192, P=None, max_persons=5, img_seed=4321,
+               desc="C3: batch {B}, {H}x{W}x3, no boxes: person detector (pooled 1x1 heads, anchor decode, conf 0.3, "
+                    "NMS 0.3, max 5) + heatmap head + soft-argmax + KEYPOINT_HEAD per detected ROI"),
+    "C4": dict(B=256, H=256, W=192, P=None, max_persons=5, img_seed=4321,
+               desc="C4: the C3 pipeline sharded {B} images/rank over {N} GPUs (global batch {G}; 2048 at 8 GPUs), "
+                    "RCCL all_gather of keypoints / visibilities / KEYPOINT_HEAD outputs / boxes / box scores every "
+                    "step"),
+    "C5": dict(B=256, H=384, W=288, P=5, max_persons=5, img_seed=1234, box_seed=1235,
+               desc="C5: {B} images/rank ({N} GPU(s), global batch {G}; 2048 at 8 GPUs), {H}x{W}x3, 5 given boxes/img, "
+                    "heatmap head + soft-argmax + KEYPOINT_HEAD per box"
+                    "{gather}"),
+}
+# outputs collated over ranks (dll.distributed.collate_outputs) for each config
+COLLATE_KEYS = {"C3": ("keypoints", "visibilities", "kh_keypoints", "kh_visibilities", "box_scores", "boxes"),
+                "C5": ("keypoints", "visibilities", "kh_keypoints", "kh_visibilities")}
+COLLATE_KEYS["C4"] = COLLATE_KEYS["C3"]
 
 
-def run_c3(a, dev, pmc, cpu=True):
-    """BASELINE config C3 on this GPU: B=256 synthetic 256x192 images without
-    boxes -> person detector (build-defined glue: pooled 1x1 heads, anchor
-    decode, threshold 0.3, NMS 0.3, max 5 kept) -> heatmap head + soft-argmax
-    and KEYPOINT_HEAD on every detected ROI.  Timed like the headline: W
-    warm-ups, K single-stream forwards with HIP events around the dominant
-    MFMA stage only; then the same at `--alt-streams` sub-batch streams
-    (throughput only).  CPU baseline: the oracle's full C3 forward (its own FPN
-    level 0 -> its detector -> dual head) on the first `--c3-cpu-sample`
-    images, 3 warm-ups + median of 5."""
-    from dll import _native
-    from dll.configs import KeypointHeadConfig, ModelConfig, TrainingConfig
-    from dll.models import MultiPersonKeypointModel
-    from dll.models.synthetic import synthetic_images, synthetic_state_dict
-    B, H, W = C3["B"], C3["H"], C3["W"]
-    m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
-                                 TrainingConfig(), precision=a.precision, dual_head=True,
-                                 max_persons=C3["max_persons"], streams=1)
-    sd = synthetic_state_dict(m.state_dict(), seed=0)
-    m.load_state_dict(sd)
-    m = m.to(dev).eval()
-    img_cpu = synthetic_images(B, 3, H, W, seed=4321)
-    img = img_cpu.to(dev)
-    plan = m.native_plan(dev)
+def slab_sums(t, total, world):
+    """float64 sum of each rank's [start, stop) image slab of a collated tensor."""
+    from dll.distributed import shard_range
+    return torch.stack([t[s:e].double().sum() for s, e in (shard_range(total, world, r) for r in range(world))])
+
+
+def collation_check(local, coll, keys, P, world, rank, dist, dev):
+    """Every rank's slab landed at its shard's offset in every rank's collated
+    copy: each rank's local (padded) outputs are summed per key in float64,
+    all_gathered, and compared with the sums of the collated slabs; the
+    verdict is AND-reduced over ranks (1 = all ranks agree)."""
+    import torch.distributed as tdist
+    from dll.distributed import pad_persons
+    mine = torch.stack([pad_persons(local[k], P).double().sum() for k in keys]).to(dev)
+    allv = [torch.empty_like(mine) for _ in range(world)]
+    tdist.all_gather(allv, mine)
+    total = coll[keys[0]].size(0)
+    ok = all(torch.equal(slab_sums(coll[k], total, world).to(dev), torch.stack([a[i] for a in allv]))
+             for i, k in enumerate(keys))
+    flag = torch.tensor([1 if ok else 0], device=dev, dtype=torch.int32)
+    tdist.all_reduce(flag, op=tdist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
+def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, standin=False):
+    """One BASELINE pipeline config on this rank's GPU (C3 / C4 / C5; see
+    PIPELINES), the dual head on every ROI.  Timed like the headline: W
+    warm-ups, K forwards between barriers (max over ranks; at N > 1 each step
+    also all-gathers the collated outputs over RCCL), HIP events around the
+    dominant MFMA stage only; its roofline traffic from the PMC entry of the
+    same per-GPU workload.  N = 1, rank 0: CPU baseline = the oracle's forward
+    of the same config on the first --cfg-cpu-sample images (3 warm-ups +
+    median of 5) and parity against it; C3 also at --alt-streams sub-batch
+    streams (throughput only).  standin: gloo ranks on the CPU with
+    StandinModel (launcher / collation test, no measurement)."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+    c = PIPELINES[name]
+    B = a.cfg_batch or c["B"]
+    H, W, P, Pk = c["H"], c["W"], c["P"], c["max_persons"]
+    detect = P is None
+    gather = dist and not a.no_gather
+    keys = COLLATE_KEYS[name]
+    img_cpu = synthetic_images(B, 3, H, W, seed=c["img_seed"] + 7919 * rank)
+    box_cpu = None if detect else synthetic_boxes(B, P, seed=c["box_seed"] + 7919 * rank)
+    if standin:
+        m = StandinModel(offset=rank * B, max_persons=Pk)
+        img = img_cpu
+        sync = (lambda: None)
+    else:
+        from dll.configs import KeypointHeadConfig, ModelConfig, TrainingConfig
+        from dll.models import MultiPersonKeypointModel
+        m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
+                                     TrainingConfig(), precision=a.precision, dual_head=True, max_persons=Pk,
+                                     streams=1)
+        m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
+        m = m.to(dev).eval()
+        img = img_cpu.to(dev)
+        sync = _cuda_sync
+    batch = img if detect else {"image": img, "bboxes": box_cpu.to(img.device)}
+    coll = {}
 
     def step():
-        return m(img)           # plain tensor: the detector branch
+        out = m(batch)
+        if gather:   # result collation over RCCL (P = max_persons on every rank: no host sync)
+            if "boxes" in keys:
+                out["boxes_t"] = torch.stack(out["boxes"])
+            src = {k: out["boxes_t" if k == "boxes" else k] for k in keys}
+            from dll.distributed import collate_outputs
+            coll.update(collate_outputs(src, B * world, keys=keys, max_persons=Pk))
+        return out
 
-    with torch.no_grad():
-        for _ in range(a.warmup):
-            step()
-    bd = stage_pass(m, plan, img, 1)
-    launches = {k: v[1] for k, v in bd.items()}
-    mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
-    dom = max((k for k in bd if k in mfma_stages), key=lambda k: bd[k][0])
-    plan.timing(True, stage=dom)
-    el, out = run_steps(a.steps, 0, step, False)
-    plan.timing(False)
-    dms, dn = plan.timing_query(dom)
-    stages = {k: v[0] for k, v in bd.items()}
+    gN = B * world
+    res = {"workload": c["desc"].format(B=B, H=H, W=W, N=world, G=gN,
+                                        gather=", RCCL all_gather of keypoints / visibilities / KEYPOINT_HEAD "
+                                               "outputs every step" if gather else ""),
+           "images_per_rank": B, "global_batch": gN, "n_gpus": world, "precision": a.precision}
+    if standin:
+        el, out = run_steps(a.steps, a.warmup, step, dist, sync=sync)
+        stages, dom = {}, None
+    else:
+        from dll import _native  # noqa: F401
+        plan = m.native_plan(dev)
+        with torch.no_grad():
+            for _ in range(a.warmup):
+                step()
+        bd = stage_pass(m, plan, batch, 1)
+        launches = {k: v[1] for k, v in bd.items()}
+        mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
+        dom = max((k for k in bd if k in mfma_stages), key=lambda k: bd[k][0])
+        plan.timing(True, stage=dom)
+        el, out = run_steps(a.steps, 0, step, dist)
+        plan.timing(False)
+        dms, dn = plan.timing_query(dom)
+        stages = {k: v[0] for k, v in bd.items()}
+        if dn:
+            stages[dom] = dms / dn
+    per_rank = gather_elapsed(el, world, dist, dev)
+    el = max(per_rank)
+    res.update({"value": round(gN * a.steps / el, 2), "unit": "images/s", "ms_per_step": round(el / a.steps * 1e3, 4),
+                "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+                "steps": a.steps, "warmup": a.warmup, "streams_per_gpu": 1, "scaling": "weak"})
+    if gather:
+        res["collated"] = {k: list(v.shape) for k, v in coll.items()}
+        res["collated_ok"] = collation_check(out if "boxes" not in keys else dict(out, boxes=out["boxes_t"]),
+                                             coll, keys, Pk, world, rank, dist, dev)
+        res["collective"] = ("all_gather over " + ("gloo (CPU stand-in)" if standin else "RCCL (nccl backend)") +
+                             f" of {', '.join(keys)} per step, padded to {Pk} persons")
+    if standin:
+        if gather:   # the stand-in encodes the global image index: every slab at its offset
+            idx = torch.arange(gN, dtype=torch.float32)
+            res["collated_index_ok"] = bool(torch.equal(coll["keypoints"][:, :, 0, :, 0],
+                                                        (idx / 1e4).view(gN, 1, 1).expand(gN, Pk, 17)))
+        return res
+    rois = int((out["box_scores"] > 0).sum()) if detect else int((box_cpu.abs().sum(-1) > 0).sum())
+    P_eff = rois / B                     # persons per image the heads ran on
     nl = max(1, launches[dom])           # launches of a stage per forward (one per pass)
-    if dn:
-        stages[dom] = dms / dn
-    rois = int((out["box_scores"] > 0).sum())
-    P_eff = rois / B                     # detected persons per image (the heads run on these ROIs)
-    fl = config_flops(H, W, P_eff, True)
-    roof = roofline(a.precision, stages, fl, B / nl, H, W, pmc, dom, tag="C3")
+    fl = config_flops(H, W, P_eff, detect)
+    tag = "C3" if name == "C4" else name   # C4's per-GPU work is C3's: its single-GPU PMC entry
+    roof = roofline(a.precision, stages, fl, B / nl, H, W, pmc, dom, tag=tag)
     roof["launches_timed"] = dn
     roof["images_per_launch"] = B / nl
     roof["rois_per_launch"] = rois / nl
     roof["timing"] = "HIP events around every launch of this stage inside the timed region (single stream)"
-    res = {"workload": f"C3: batch {B}, {H}x{W}x3, no boxes: person detector (pooled 1x1 heads, anchor decode, "
-                       f"conf 0.3, NMS 0.3, max {C3['max_persons']}) + heatmap head + soft-argmax + KEYPOINT_HEAD "
-                       "per detected ROI",
-           "value": round(B * a.steps / el, 2), "unit": "images/s", "ms_per_step": round(el / a.steps * 1e3, 4),
-           "steps": a.steps, "warmup": a.warmup, "streams_per_gpu": 1, "precision": a.precision,
-           "rois": rois, "persons_per_image": round(P_eff, 3),
-           "gflop_per_image": round(fl["total"] / 1e9, 3),
-           "achieved_tflops_total": round(fl["total"] * B * a.steps / el / 1e12, 2),
-           "roofline": roof, "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-           "stage_launches_per_forward": launches}
+    if name == "C4":
+        roof["pmc_note"] = "traffic / busy: the single-GPU C3 PMC entry (C4's per-rank workload is C3's)"
+    res.update({"rois": rois, "persons_per_image": round(P_eff, 3), "gflop_per_image": round(fl["total"] / 1e9, 3),
+                "achieved_tflops_total": round(fl["total"] * gN * a.steps / el / 1e12, 2), "roofline": roof,
+                "stages_ms": {k: round(v, 4) for k, v in stages.items()}, "stage_launches_per_forward": launches})
     if "keypoint_head" in stages:
         # the keypoint_head stage runs the KEYPOINT_HEAD convs, pools and linears; its spatial attention
         # (1x1 128->64->1) is fused into the roi_align stage's kernel (roi_kh_kernel) in split precision
@@ -494,7 +605,7 @@ def run_c3(a, dev, pmc, cpu=True):
         res["keypoint_head_note"] = ("algorithmic KEYPOINT_HEAD flops of the keypoint_head stage / its time"
                                      + ("; the spatial attention's 1x1 convs run fused in the roi_align stage"
                                         if fused else ""))
-    if a.alt_streams and a.alt_streams != 1:
+    if name == "C3" and world == 1 and a.alt_streams and a.alt_streams != 1:
         m.streams = a.alt_streams
         el2, out2 = run_steps(a.steps, a.warmup, step, False)
         m.streams = 1
@@ -503,41 +614,60 @@ def run_c3(a, dev, pmc, cpu=True):
                               "outputs_identical": all(torch.equal(out[k], out2[k]) for k in
                                                        ("keypoints", "visibilities", "kh_keypoints",
                                                         "box_scores"))}
-    if cpu and a.c3_cpu_sample > 0:
+    if cpu and world == 1 and rank == 0 and a.cfg_cpu_sample > 0:
         from oracle import kpd_oracle as O
         ci = host_cpu_info()
-        S = min(a.c3_cpu_sample, B)
+        S = min(a.cfg_cpu_sample, B)
         sdc = {k: v.cpu() for k, v in m.state_dict().items()}
         xs = img_cpu[:S]
+        bs = None if detect else box_cpu[:S]
 
         def fwd():
-            return O.forward(sdc, {"image": xs}, dual_head=True,
-                             detect=dict(conf_threshold=0.3, iou_threshold=0.3, max_persons=C3["max_persons"]))
-        ref, rate, proto = cpu_baseline(sdc, xs, None, ci["threads"], fwd=fwd)
+            if detect:
+                return O.forward(sdc, {"image": xs}, dual_head=True,
+                                 detect=dict(conf_threshold=0.3, iou_threshold=0.3, max_persons=Pk))
+            return O.forward(sdc, {"image": xs, "bboxes": bs}, dual_head=True)
+        ref, rate, proto = cpu_baseline(sdc, xs, bs, ci["threads"], fwd=fwd)
+        what = ("its own FPN level 0 -> detector glue -> heatmap head + KEYPOINT_HEAD" if detect else
+                "the reference's per-box loop -> heatmap head + KEYPOINT_HEAD")
         res["cpu_baseline"] = {
             "value": round(rate, 3), "unit": "images/s", "cores": ci["threads"], "kind": "port",
-            "sample": f"{S} images of the same C3 workload, oracle/kpd_oracle.py (its own FPN level 0 -> detector "
-                      f"glue -> heatmap head + KEYPOINT_HEAD), {proto['warmups']} warmups + median of "
-                      f"{proto['runs']} runs",
+            "sample": f"{S} images of the same {name} workload, oracle/kpd_oracle.py ({what}), "
+                      f"{proto['warmups']} warmups + median of {proto['runs']} runs",
             "protocol": proto, "cpu_model": ci["model"]}
         res["gpu_vs_cpu"] = round(res["value"] / rate, 1)
-        gb = torch.stack([out["boxes"][i].cpu() for i in range(S)])
         gk = out["keypoints"][:S].cpu()
         d = (gk - ref["keypoints"]).norm(dim=-1)
-        res["parity"] = {
-            "images": S, "pck@0.5": float((d <= 0.5).float().mean()), "pck@0.002": float((d <= 0.002).float().mean()),
-            "max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
-            "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
-            "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
-            "max_abs_dkh_kpt": float((out["kh_keypoints"][:S].cpu() - ref["kh_keypoints"]).abs().max()),
-            "max_abs_dkh_vis": float((out["kh_visibilities"][:S].cpu() - ref["kh_visibilities"]).abs().max()),
-            "kept_persons_equal": bool(torch.equal((out["box_scores"][:S].cpu() > 0).sum(1),
-                                                   (ref["box_scores"] > 0).sum(1))),
-            "max_abs_dbox": float((gb - torch.stack(list(ref["boxes"]))).abs().max()),
-            "max_abs_dscore": float((out["box_scores"][:S].cpu() - ref["box_scores"]).abs().max())}
+        par = {"images": S, "pck@0.5": float((d <= 0.5).float().mean()),
+               "pck@0.002": float((d <= 0.002).float().mean()),
+               "max_abs_dkpt": float((gk - ref["keypoints"]).abs().max()),
+               "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
+               "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
+               "max_abs_dkh_kpt": float((out["kh_keypoints"][:S].cpu() - ref["kh_keypoints"]).abs().max()),
+               "max_abs_dkh_vis": float((out["kh_visibilities"][:S].cpu() - ref["kh_visibilities"]).abs().max()),
+               "kh_vis_argmax_flips": int((out["kh_visibilities"][:S].cpu().argmax(-1)
+                                           != ref["kh_visibilities"].argmax(-1)).sum())}
+        if detect:
+            gb = torch.stack([out["boxes"][i].cpu() for i in range(S)])
+            par.update({"kept_persons_equal": bool(torch.equal((out["box_scores"][:S].cpu() > 0).sum(1),
+                                                               (ref["box_scores"] > 0).sum(1))),
+                        "max_abs_dbox": float((gb - torch.stack(list(ref["boxes"]))).abs().max()),
+                        "max_abs_dscore": float((out["box_scores"][:S].cpu() - ref["box_scores"]).abs().max())})
+        res["parity"] = par
     del m, plan, out
     torch.cuda.empty_cache()
     return res
+
+
+def config_names(a, world):
+    """Labelled config objects of this run: N = 1: C3 + C5; N > 1: C4 + C5."""
+    if a.only:
+        return [a.only]
+    if a.configs == "none":
+        return []
+    if a.configs == "auto":
+        return ["C3", "C5"] if world == 1 else ["C4", "C5"]
+    return [x for x in a.configs.split(",") if x]
 
 
 def kernel_src_hash():
@@ -587,9 +717,12 @@ def main(argv=None):
             pmc = json.loads(pj.read_text())
         except ValueError:
             pmc = None
-    if a.c3_only:
+    if a.only:
+        res = run_pipeline(a.only, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline)
         if rank == 0:
-            print(json.dumps({"configs": {"C3": run_c3(a, dev, pmc, cpu=not a.no_cpu_baseline)}}), flush=True)
+            print(json.dumps({"configs": {a.only: res}}), flush=True)
+        if dist:
+            tdist.destroy_process_group()
         return
 
     def build(precision):
@@ -727,11 +860,14 @@ def main(argv=None):
                           "max_abs_dheat": float((out["heatmap"][:S].cpu() - ref["heatmap"]).abs().max()),
                           "vis_flips": int((out["visibilities"][:S].cpu() != ref["visibilities"]).any(-1).sum()),
                           "images": S}
-    if world == 1 and a.c3:
-        # BASELINE C3 (the north_star's full pipeline) as a labelled object beside the C2 headline
+    names = config_names(a, world)
+    if names:
+        # the north_star's full pipeline (C3 at N=1, C4 at N>1) and C5 as labelled objects beside the C2
+        # headline, on the same ranks
         del m, plan
         torch.cuda.empty_cache()
-        line["configs"] = {"C3": run_c3(a, dev, pmc, cpu=not a.no_cpu_baseline)}
+        line["configs"] = {n: run_pipeline(n, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline)
+                           for n in names}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

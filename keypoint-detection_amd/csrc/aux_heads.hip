@@ -22,7 +22,11 @@
 namespace {
 constexpr int G = 56, GP = G * G, NA = 9;
 
-// [B][Hf][Wf][C] -> [B][56][56][C], PyTorch adaptive_avg_pool2d bins; thread per (cell, channel quad)
+// [B][Hf][Wf][C] -> [B][56][56][C], PyTorch adaptive_avg_pool2d bins; thread per (cell, channel quad).
+// Summed as person_detect_kernel sums (column sums over y, then over x), so
+// the pooled features of the KPD_PD_UNFUSED diagnostic path round exactly as
+// the fused default's; its 1x1 heads (conv_mfma) still sum K in another order,
+// so the two paths' scores agree to fp32 rounding, not bit for bit.
 __global__ __launch_bounds__(256) void adaptive_pool56_kernel(const float* __restrict__ in, int B, int Hf, int Wf,
                                                               int C, float* __restrict__ out) {
   const int nq = C / 4;
@@ -34,11 +38,14 @@ __global__ __launch_bounds__(256) void adaptive_pool56_kernel(const float* __res
   const int y0 = (i * Hf) / G, y1 = ((i + 1) * Hf + G - 1) / G;
   const int x0 = (j * Wf) / G, x1 = ((j + 1) * Wf + G - 1) / G;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int y = y0; y < y1; ++y)
-    for (int x = x0; x < x1; ++x) {
+  for (int x = x0; x < x1; ++x) {
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int y = y0; y < y1; ++y) {
       const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)b * Hf + y) * Wf + x) * C + q * 4);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      cs.x += v.x; cs.y += v.y; cs.z += v.z; cs.w += v.w;
     }
+    s.x += cs.x; s.y += cs.y; s.z += cs.z; s.w += cs.w;
+  }
   const float cnt = (float)((y1 - y0) * (x1 - x0));
   *reinterpret_cast<float4*>(out + cell * C + q * 4) = make_float4(s.x / cnt, s.y / cnt, s.z / cnt, s.w / cnt);
 }

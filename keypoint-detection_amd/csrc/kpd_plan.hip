@@ -238,7 +238,11 @@ struct kpd_plan {
   // call signature (shapes, flags, every buffer address, stream), valid while
   // the workspace carve and the weights are the ones it was captured on
   // never: instantiation failed for this signature -> always eager
-  struct GraphEntry { hipGraphExec_t exec = nullptr; long epoch = -1; int seen = 0; bool never = false; };
+  // done: recorded after each launch of exec on its caller's stream; retiring
+  // an entry waits on it (not on the whole device) before destroying exec
+  struct GraphEntry {
+    hipGraphExec_t exec = nullptr; hipEvent_t done = nullptr; long epoch = -1; int seen = 0; bool never = false;
+  };
   std::map<std::vector<uintptr_t>, GraphEntry> graphs;
   long ws_epoch = 0;             // bumped whenever a workspace is re-carved or the weights re-packed
   bool use_graphs = getenv("KPD_GRAPH") != nullptr && atoi(getenv("KPD_GRAPH")) != 0;   // kpd_plan_set_graphs (KPD_GRAPH=1: on)
@@ -883,6 +887,20 @@ int kpd_plan_set_tensor(kpd_plan* p, const char* name, const float* host, const 
   return KPD_OK;
 }
 
+// wait for a captured forward's last launch (its own event, not the device),
+// then destroy it
+static hipError_t retire_graph(kpd_plan::GraphEntry& g) {
+  hipError_t e = hipSuccess;
+  if (g.done) {
+    e = hipEventSynchronize(g.done);
+    (void)hipEventDestroy(g.done);
+    g.done = nullptr;
+  }
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  g.exec = nullptr;
+  return e;
+}
+
 void kpd_plan_destroy(kpd_plan* p) {
   if (!p) return;
   int cur = 0;
@@ -897,8 +915,7 @@ void kpd_plan_destroy(kpd_plan* p) {
     if (p->pipe_ev[k]) (void)hipEventDestroy(p->pipe_ev[k]);
   }
   if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
-  for (auto& kv : p->graphs)
-    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  for (auto& kv : p->graphs) (void)retire_graph(kv.second);
   if (p->graph_st) (void)hipStreamDestroy(p->graph_st);
   for (auto& kv : p->timers)
     for (auto& e : kv.second.ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -1711,6 +1728,14 @@ static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, in
                         int flags, float* kpts, float* vis, float* heat, float* kh_kpts, float* kh_vis,
                         float* box_scores, int32_t* topk_out, void* stream);
 
+// launch a captured forward on the caller's stream and mark its completion
+static int launch_graph(kpd_plan::GraphEntry& g, hipStream_t st) {
+  HIP_TRY(hipGraphLaunch(g.exec, st));
+  if (!g.done) HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(g.done, st));
+  return KPD_OK;
+}
+
 // KPD_GRAPH=1: a forward is a launch-bound chain of ~60 kernels (at one image
 // the launches, not the kernels, set the latency), so a repeated call with the
 // same signature replays one captured hipGraph.  The first call of a
@@ -1734,11 +1759,10 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
                         topk_out, s_);
   };
   if (p->graphs.size() >= 64 && !p->graphs.count(key)) {   // signatures that never repeat: bounded
-    // the executable graphs may still be running on their callers' streams
+    // the executable graphs may still be running on their callers' streams:
+    // each waits for its own last launch only
     HIP_TRY(hipSetDevice(p->device));
-    HIP_TRY(hipDeviceSynchronize());
-    for (auto& kv : p->graphs)
-      if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    for (auto& kv : p->graphs) HIP_TRY(retire_graph(kv.second));
     p->graphs.clear();
   }
   kpd_plan::GraphEntry& g = p->graphs[key];
@@ -1754,14 +1778,11 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
         HIP_TRY(hipMemsetAsync(p->work[k].sc, 0, (size_t)2 * p->dims[k].B * kAmaxStride * sizeof(float), st));
         p->work[k].sc_dirty = false;
       }
-    HIP_TRY(hipGraphLaunch(g.exec, st));
-    return KPD_OK;
+    return launch_graph(g, st);
   }
-  if (g.exec) {   // stale (re-carve, re-finalize, detector change): it may still be running
+  if (g.exec) {   // stale (re-carve, re-finalize, detector change): its last launch may still be running
     HIP_TRY(hipSetDevice(p->device));
-    HIP_TRY(hipDeviceSynchronize());
-    (void)hipGraphExecDestroy(g.exec);
-    g.exec = nullptr;
+    HIP_TRY(retire_graph(g));
     g.seen = 0;
   }
   if (g.seen++ == 0)   // eager: allocations and first-use setup happen outside any capture
@@ -1816,8 +1837,7 @@ int kpd_forward(kpd_plan* p, const float* image, int B, int C, int H, int W, flo
   }
   g.exec = exec;
   g.epoch = p->ws_epoch;
-  HIP_TRY(hipGraphLaunch(g.exec, st));
-  return KPD_OK;
+  return launch_graph(g, st);
 }
 
 static int forward_impl(kpd_plan* p, const float* image, int B, int C, int H, int W, float* boxes, int NB, int P,

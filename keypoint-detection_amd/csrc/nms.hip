@@ -247,7 +247,10 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
       if (pass == 0 && sh_cnt > kNmsList) break;   // (cannot happen: keys > tau number < kNmsPrefix)
     }
     int m = sh_cnt;
-    const bool all = m == (int)total;           // S holds every alive candidate
+    // S holds every alive candidate and fits the list.  Decided before the
+    // re-compaction below: after a tie overflow the list holds only keys > tau,
+    // a strict prefix, so running dry there must fall back to the full pass.
+    const bool covered = m == (int)total && m <= kNmsList;
     if (m > kNmsList) {                         // the ties overflowed: keep only keys > tau (a prefix too)
       __syncthreads();
       if (tid == 0) sh_cnt = 0;
@@ -261,7 +264,6 @@ __global__ __launch_bounds__(1024) void nms_reg_kernel(const float* __restrict__
       __syncthreads();
       m = sh_cnt;
     }
-    const bool covered = all && m <= kNmsList;
     // greedy rounds over the list: thread t holds entries t and t + 1024
     constexpr int PER = kNmsList / 1024;
     int li[PER];

@@ -448,10 +448,15 @@ def box_iou_cxcywh(b1: Tensor, b2: Tensor) -> Tensor:
 
 
 def nms(boxes: Tensor, scores: Tensor, iou_threshold: float = 0.2,
-        max_output_size: Optional[int] = None) -> Tensor:
+        max_output_size: Optional[int] = None, stable: bool = False) -> Tensor:
     """Greedy NMS exactly as person_head.py:96-139 (IoU > thr suppressed; the
-    sort order of ``scores.sort(descending=True)`` decides ties)."""
-    _, order = scores.sort(0, descending=True)
+    sort order of ``scores.sort(descending=True)`` decides ties).  stable=True
+    breaks ties by the lower index (a stable sort: one of the orders the
+    reference's unstable sort may produce, and the one the HIP kernel uses)."""
+    if stable:
+        _, order = torch.sort(scores, dim=0, descending=True, stable=True)
+    else:
+        _, order = scores.sort(0, descending=True)
     keep: List[int] = []
     while order.numel() > 0:
         if order.numel() == 1:

@@ -27,7 +27,12 @@ def _line(stdout):
 
 
 def test_bench_gpus2_launches_two_ranks():
-    r = _run(["--gpus", "2", "--cpu-standin", "--steps", "3", "--warmup", "1", "--batch", "6", "--persons", "2"])
+    """N = 2: the C2 headline plus the C4 (C3 pipeline per rank, detector
+    outputs collated) and C5 (given boxes, dual head) objects, each timed
+    between barriers with the max over ranks and every rank's slab found at
+    its shard's offset in the collated outputs."""
+    r = _run(["--gpus", "2", "--cpu-standin", "--steps", "3", "--warmup", "1", "--batch", "6", "--persons", "2",
+              "--cfg-batch", "3"])
     assert r.returncode == 0, r.stderr[-3000:]
     line = _line(r.stdout)
     assert line["n_gpus"] == 2 and line["world"] == 2 and line["backend"] == "gloo"
@@ -36,13 +41,26 @@ def test_bench_gpus2_launches_two_ranks():
     assert line["collated"]["keypoints"] == [12, 2, 1, 17, 2]
     assert line["collated"]["visibilities"] == [12, 2, 1, 17, 3]
     assert line["collated_ok"] is True
+    cfg = line["configs"]
+    assert sorted(cfg) == ["C4", "C5"]
+    c4, c5 = cfg["C4"], cfg["C5"]
+    for c in (c4, c5):
+        assert c["n_gpus"] == 2 and c["global_batch"] == 6 and c["images_per_rank"] == 3
+        assert len(c["rank_ms_per_step"]) == 2 and c["ms_per_step"] == max(c["rank_ms_per_step"])
+        assert c["collated_ok"] is True and c["collated_index_ok"] is True
+        assert c["collated"]["keypoints"] == [6, 5, 1, 17, 2]
+        assert c["collated"]["kh_visibilities"] == [6, 5, 1, 17, 3]
+    assert c4["collated"]["boxes"] == [6, 5, 4] and c4["collated"]["box_scores"] == [6, 5]
+    assert "boxes" not in c5["collated"] and "384x288" in c5["workload"]
 
 
 def test_bench_gpus1_single_process():
-    r = _run(["--gpus", "1", "--cpu-standin", "--steps", "2", "--warmup", "0", "--batch", "4"])
+    r = _run(["--gpus", "1", "--cpu-standin", "--steps", "2", "--warmup", "0", "--batch", "4", "--cfg-batch", "2"])
     assert r.returncode == 0, r.stderr[-3000:]
     line = _line(r.stdout)
     assert line["n_gpus"] == 1 and line["world"] == 1 and line["collated"] == {}
+    assert sorted(line["configs"]) == ["C3", "C5"]
+    assert all("collated" not in c for c in line["configs"].values())
 
 
 def test_bench_gpus_mismatch_fails():

@@ -303,6 +303,24 @@ def test_nms_prefix_paths():
     ref = O.nms(boxes, tied, 0.3, 600)
     assert got.numel() == ref.numel()
     assert torch.equal(tied[got], tied[ref])
+    # ties beyond the LDS list when the prefix holds every alive candidate
+    # (ADVICE r4): all 3,000 scores equal -> the list re-compacts to the keys
+    # above tau (none) and must fall back to the full pass, not stop empty
+    b3 = boxes[:3000].contiguous()
+    eq = torch.full((3000,), 0.6)
+    for mo in (5, 0):
+        got = _native.nms(b3.to(DEV), eq.to(DEV), 0.3, mo).cpu()
+        ref = O.nms(b3, eq, 0.3, mo if mo > 0 else None, stable=True)
+        assert got.numel() > 0 and torch.equal(got, ref), mo
+    # 500 distinct scores above 2,600 ties at the lowest score: the kept boxes
+    # must run on into the ties
+    b4 = boxes[:3100].contiguous()
+    s4 = torch.full((3100,), 0.4)
+    s4[:500] = 0.5 + 0.4 * torch.randperm(500, generator=g).float() / 500
+    got = _native.nms(b4.to(DEV), s4.to(DEV), 0.3, 600).cpu()
+    ref = O.nms(b4, s4, 0.3, 600, stable=True)
+    assert torch.equal(got, ref)
+    assert (s4[got] == 0.4).any()
 
 
 def _dual_model(precision="fp32"):
