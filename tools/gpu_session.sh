@@ -14,6 +14,7 @@
 #   ab      same-box A/B of diagnostic switches on libkpd_diag.so (make diag):
 #           AB_ENVS="NAME=1;NAME2=1" (";"-separated variants, "-" = none), AB_CFG c2|c3|c5
 #   stamps  KPD_STAMPS phase stamps of the heatmap convs (diag build)
+#   bstamps KPD_STAMPS phase stamps of the body kernels (tools/stamps_probe.py, diag build)
 #   grad    K6 backward timing at the heatmap conv 2 shape
 set -u
 ROOTD="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -119,6 +120,11 @@ print(sys.argv[2], "value", c["value"], "ms", c["ms_per_step"], {k: round(v, 3) 
 PY
       done
     done ;;
+  bstamps)
+    # body / lateral-chain / ROI-align per-workgroup phase stamps (tools/stamps_probe.py)
+    env KPD_DIAG_LIB=1 KPD_STAMPS=1 timeout -k 10 180 python3 tools/stamps_probe.py > "$OUT/stamps_body.txt" 2>&1 \
+      || { echo "bstamps rc=$?"; tail -5 "$OUT/stamps_body.txt"; exit 1; }
+    cat "$OUT/stamps_body.txt" | cut -c1-220 | head -120 ;;
   stamps)
     for k in ${STAMP_SETS:-stamps_hm1 stamps_hm2 stamps_hm3}; do
       env KPD_DIAG_LIB=1 KPD_STAMPS=1 timeout -k 10 120 python3 tools/stamps_hm2.py $k split \
