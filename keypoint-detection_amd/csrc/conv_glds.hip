@@ -575,9 +575,7 @@ __global__ __launch_bounds__(NT) void conv16_kernel(const Conv16Args p) {
 // rows / columns outside the grid).  Register epilogue with the channel
 // statistics; rows past the image's class grid are masked out of them.
 // DBG (ablations, KPD_FPN0X_DBG; wrong results by design): 1 = no MFMA, 2 = no K-loop DMA,
-// 4 = output stores of one piece only (the others go to an out-of-range offset);
-// L2 policy A/B (results unchanged): 8 = tap0 / lateral-1 rows loaded
-// non-temporal, 16 = the weights non-temporal
+// 4 = output stores of one piece only (the others go to an out-of-range offset)
 template <int DBG>
 __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
   constexpr int BN = 128, S = 3, WAVES_N = 2, WAVES_M = 4;
@@ -743,11 +741,11 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const unsigned voff = (t < 9 && ((mk[i] >> t) & 1u)) ? fo[i] + delta : OOB;
-      glds16p<(DBG & 8) != 0>(rf, a_dst + so + i * 8 * ROWB, voff, 0);
+      glds16(rf, a_dst + so + i * 8 * ROWB, voff, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i)
-      glds16p<(DBG & 16) != 0>(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + k) * ROWB + lchunk * 16), 0);
+      glds16(rw0, b_dst + so + i * 8 * ROWB, (unsigned)(((co_b + i * 8) * KT0 + k) * ROWB + lchunk * 16), 0);
   };
   auto issue = [&](int stage) {
     const unsigned so = stage * STAGE;
@@ -760,12 +758,12 @@ __global__ __launch_bounds__(NT) void fpn0x_kernel(const Fpn0xArgs p) {
 #pragma unroll
       for (int i = 0; i < A_LD; ++i) {
         const unsigned voff = ((mask[i] >> (9 + g)) & 1u) ? l_off[i] + delta : OOB;
-        glds16p<(DBG & 8) != 0>(rl, a_dst + so + i * 8 * ROWB, voff, 0);
+        glds16(rl, a_dst + so + i * 8 * ROWB, voff, 0);
       }
       const int wbase = s_woff[cls] * 2;   // bytes
 #pragma unroll
       for (int i = 0; i < B_LD; ++i)
-        glds16p<(DBG & 16) != 0>(rwe, b_dst + so + i * 8 * ROWB,
+        glds16(rwe, b_dst + so + i * 8 * ROWB,
                (unsigned)(wbase + (((co_b + i * 8) * NG + g) * 4 + kc) * ROWB + lchunk * 16), 0);
     }
     ++ld;
@@ -2311,9 +2309,6 @@ hipError_t launch_fpn0x(const Fpn0xArgs& a, hipStream_t st) {
   if (dbg == 1) hipLaunchKernelGGL(fpn0x_kernel<1>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 2) hipLaunchKernelGGL(fpn0x_kernel<2>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else if (dbg == 4) hipLaunchKernelGGL(fpn0x_kernel<4>, dim3((unsigned)grid), dim3(NT), 0, st, b);
-  else if (dbg == 8) hipLaunchKernelGGL(fpn0x_kernel<8>, dim3((unsigned)grid), dim3(NT), 0, st, b);
-  else if (dbg == 16) hipLaunchKernelGGL(fpn0x_kernel<16>, dim3((unsigned)grid), dim3(NT), 0, st, b);
-  else if (dbg == 24) hipLaunchKernelGGL(fpn0x_kernel<24>, dim3((unsigned)grid), dim3(NT), 0, st, b);
   else
 #endif
   hipLaunchKernelGGL(fpn0x_kernel<0>, dim3((unsigned)grid), dim3(NT), 0, st, b);

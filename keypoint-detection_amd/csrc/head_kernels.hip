@@ -251,6 +251,36 @@ __device__ __forceinline__ void roi_row_sample(const float* __restrict__ feat, i
       if (iy) __syncthreads();   // every bin finished reading the previous row's T
       const float* r1 = fb + (size_t)yl * Wf * Cf;
       const float* r2 = fb + (size_t)yh * Wf * Cf;
+      if (topk == nullptr && Cf == CO) {
+        // every channel in order (CW 2: the 128-channel KEYPOINT_HEAD rows):
+        // 16-byte loads, lane = (column, channel quad), CPI columns per
+        // wave-instruction -- a quarter of the load / LDS-store instructions of
+        // the per-channel form below, the same T values
+        constexpr int QPC = CO / 4, CPI = 64 / QPC, UB4 = 4;
+        const int qd = lane % QPC, cs = lane / QPC;
+        for (int base = wave * CPI; base < nc; base += 4 * CPI * UB4) {
+          float4 v1[UB4], v2[UB4];
+#pragma unroll
+          for (int u = 0; u < UB4; ++u) {
+            const int px = min(base + u * 4 * CPI + cs, nc - 1);
+            const size_t o = (size_t)(xlo + px) * Cf + qd * 4;
+            v1[u] = *reinterpret_cast<const float4*>(r1 + o);
+            v2[u] = *reinterpret_cast<const float4*>(r2 + o);
+          }
+#pragma unroll
+          for (int u = 0; u < UB4; ++u) {
+            const int px = base + u * 4 * CPI + cs;
+            if (px < nc) {
+              float4 t;
+              t.x = yin ? hy * v1[u].x + ly * v2[u].x : 0.f;
+              t.y = yin ? hy * v1[u].y + ly * v2[u].y : 0.f;
+              t.z = yin ? hy * v1[u].z + ly * v2[u].z : 0.f;
+              t.w = yin ? hy * v1[u].w + ly * v2[u].w : 0.f;
+              *reinterpret_cast<float4*>(stage + px * CO + qd * 4) = t;
+            }
+          }
+        }
+      } else {
       // 8 columns per wave per batch, every load of a batch in flight before
       // the first use (one L2 round trip per batch instead of per column)
       constexpr int UB = 8;
@@ -273,6 +303,7 @@ __device__ __forceinline__ void roi_row_sample(const float* __restrict__ feat, i
 #pragma unroll
             for (int q = 0; q < CW; ++q) stage[px * CO + lane + TOPK * q] = yin ? hy * v1[u][q] + ly * v2[u][q] : 0.f;
         }
+      }
       }
       __syncthreads();
       if (iy == 0) stamp(1);

@@ -27,24 +27,6 @@ __device__ __forceinline__ void glds16(i32x4 rsrc, unsigned lds_dst, unsigned vo
       : "memory");
 }
 
-// glds16 with the non-temporal load hint (streaming: the line is the L2's
-// first eviction candidate), for operands read once per launch whose L2
-// residency would push out data that IS re-read (weights)
-__device__ __forceinline__ void glds16_nt(i32x4 rsrc, unsigned lds_dst, unsigned voff, int soff) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen nt lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds_dst), "v"(voff), "s"(rsrc), "s"(soff)
-      : "memory");
-}
-template <bool NT>
-__device__ __forceinline__ void glds16p(i32x4 rsrc, unsigned lds_dst, unsigned voff, int soff) {
-  if constexpr (NT) glds16_nt(rsrc, lds_dst, voff, soff);
-  else glds16(rsrc, lds_dst, voff, soff);
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt");
