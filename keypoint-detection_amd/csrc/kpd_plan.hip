@@ -1264,7 +1264,8 @@ static int run_heatmap_head(kpd_plan* p, Work& w, int R, int P, float* heat_out,
 // x_ready: the first conv's split operand (x * attention) is already in
 // w.kxs (roi_kh_kernel wrote it with the HeatmapHead's ROI align).
 static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts, float* kh_vis, hipStream_t st,
-                             const float* bound, int bdiv, int bstride, bool x_ready = false) {
+                             const float* bound, int bdiv, int bstride, bool x_ready = false,
+                             unsigned long long* const* stamps = nullptr) {
   const size_t px = (size_t)R * 3136;
   if (p->kh_split && w.kxs) {
     // fp32-accurate split products on zero-bordered maps (hmconv_kernel MODE 2):
@@ -1296,6 +1297,7 @@ static int run_keypoint_head(kpd_plan* p, Work& w, int R, int P, float* kh_kpts,
       h.split = 1; h.hsc = w.hsc; h.w_exp = k.w_exp;
       h.in_c = i == 0 ? 0.f : 6.f; h.in_s = i == 0 ? 1.f : 0.f; h.in_idx = 2;
       h.out_c = 6.f; h.out_s = 0.f; h.out_idx = k.ns > 0 ? 2 : -1; h.amax_idx = -1;
+      h.stamps = stamps ? stamps[i] : nullptr;   // (KPD_STAMPS, diagnostic build)
       HIP_TRY(launch_hmconv(h, st));
     }
     const int o = p->kh_o, kr = pad16(16 * o * o);
@@ -1719,7 +1721,11 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     // KEYPOINT_HEAD on ROI-align of the 128-channel FPN level 0 (keypoint_head.py:51-62)
     Stage sg(p, "keypoint_head", st);
     if (!roi_kh) HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
-    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1, roi_kh)) return rc;
+    const long khrows = (long)R * kHmRoiPos - kHmPitch;
+    unsigned long long* khst[3] = {take_stamps("stamps_kh1", (size_t)((khrows + 255) / 256)),
+                                   take_stamps("stamps_kh2", (size_t)((khrows + 383) / 384)),
+                                   take_stamps("stamps_kh3", (size_t)((khrows + 511) / 512))};
+    if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1, roi_kh, khst)) return rc;
   }
   return KPD_OK;
 }
