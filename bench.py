@@ -9,7 +9,10 @@ soft-argmax decode -- through the native HIP path.
 
 One process per GPU; images shard across ranks (weak scaling, B per rank) and
 each step all-gathers the per-image keypoints/visibilities to every rank over
-RCCL (result collation, BASELINE C4).  Rank 0 prints one JSON line with the
+RCCL (result collation), pipelined one step deep: step k's all_gather runs
+under step k + 1's forward, the last one completes inside the timed region.
+With N > 1 the labelled `configs.C4` (the C3 pipeline per rank) and
+`configs.C5` objects do the same for the full pipeline.  Rank 0 prints one JSON line with the
 whole-job rate, the dominant kernel's roofline fraction (HIP events on the
 launch stream, inside the timed region) and the CPU-oracle baseline timed on
 this host (N=1 only).
@@ -221,12 +224,16 @@ def _cuda_sync():
     torch.cuda.synchronize()
 
 
-def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync):
-    """W untimed + K timed steps bracketed by barrier + synchronize; seconds."""
+def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync, finish=None):
+    """W untimed + K timed steps bracketed by barrier + synchronize; seconds.
+    finish(): completes work a step leaves in flight (the last step's result
+    collation), inside the timed region, before the closing synchronize."""
     import torch.distributed as tdist
     with torch.no_grad():
         for _ in range(warmup):
             step_fn()
+        if finish:
+            finish()
         sync()
         if dist:
             tdist.barrier()
@@ -234,6 +241,8 @@ def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync):
         t0 = time.perf_counter()
         for _ in range(steps):
             out = step_fn()
+        if finish:
+            finish()
         sync()
         if dist:
             tdist.barrier()
@@ -296,6 +305,29 @@ class StandinModel:
         return out
 
 
+class Collator:
+    """Result collation pipelined one step deep: step k starts the all_gathers
+    of its outputs (async) after waiting for step k - 1's, so each step's
+    collective runs under the next step's forward instead of in series with it
+    (dll.distributed.collate_outputs(..., async_op=True)); finish() completes
+    the last one (run_steps calls it inside the timed region).  The collated
+    tensors of the latest completed step land in ``into``."""
+
+    def __init__(self, total, keys, max_persons, into):
+        self.total, self.keys, self.p, self.into, self.pending = total, keys, max_persons, into, None
+
+    def start(self, out):
+        from dll.distributed import collate_outputs
+        src = {k: out[k] for k in self.keys}
+        self.finish()
+        self.pending = collate_outputs(src, self.total, keys=self.keys, max_persons=self.p, async_op=True)
+
+    def finish(self):
+        if self.pending is not None:
+            self.into.update(self.pending.wait())
+            self.pending = None
+
+
 def main_standin(a, world, rank, dist):
     """The N-rank code path of main() with gloo on the CPU and StandinModel."""
     import torch.distributed as tdist
@@ -309,14 +341,15 @@ def main_standin(a, world, rank, dist):
     model = StandinModel()
     gather = dist and not a.no_gather
     coll = {}
+    pend = Collator(B * world, ("keypoints", "visibilities"), P, coll)
 
     def step():
         out = model(batch)
         if gather:
-            coll.update(collate_outputs(out, B * world, max_persons=P))
+            pend.start(out)
         return out
 
-    el, _ = run_steps(a.steps, a.warmup, step, dist, sync=lambda: None)
+    el, _ = run_steps(a.steps, a.warmup, step, dist, sync=lambda: None, finish=pend.finish)
     per_rank = gather_elapsed(el, world, dist, torch.device("cpu"))
     el = max(per_rank)
     line = {"metric": "cpu-standin (launcher test; not a measurement)", "value": round(B * world * a.steps / el, 2),
@@ -528,15 +561,14 @@ def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, stand
         sync = _cuda_sync
     batch = img if detect else {"image": img, "bboxes": box_cpu.to(img.device)}
     coll = {}
+    pend = Collator(B * world, keys, Pk, coll)
 
     def step():
         out = m(batch)
-        if gather:   # result collation over RCCL (P = max_persons on every rank: no host sync)
+        if gather:   # result collation over RCCL (P = max_persons on every rank: no host sync), one step deep
             if "boxes" in keys:
                 out["boxes_t"] = torch.stack(out["boxes"])
-            src = {k: out["boxes_t" if k == "boxes" else k] for k in keys}
-            from dll.distributed import collate_outputs
-            coll.update(collate_outputs(src, B * world, keys=keys, max_persons=Pk))
+            pend.start({k: out["boxes_t" if k == "boxes" else k] for k in keys})
         return out
 
     gN = B * world
@@ -545,7 +577,7 @@ def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, stand
                                                "outputs every step" if gather else ""),
            "images_per_rank": B, "global_batch": gN, "n_gpus": world, "precision": a.precision}
     if standin:
-        el, out = run_steps(a.steps, a.warmup, step, dist, sync=sync)
+        el, out = run_steps(a.steps, a.warmup, step, dist, sync=sync, finish=pend.finish)
         stages, dom = {}, None
     else:
         from dll import _native  # noqa: F401
@@ -553,12 +585,13 @@ def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, stand
         with torch.no_grad():
             for _ in range(a.warmup):
                 step()
+            pend.finish()
         bd = stage_pass(m, plan, batch, 1)
         launches = {k: v[1] for k, v in bd.items()}
         mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
         dom = max((k for k in bd if k in mfma_stages), key=lambda k: bd[k][0])
         plan.timing(True, stage=dom)
-        el, out = run_steps(a.steps, 0, step, dist)
+        el, out = run_steps(a.steps, 0, step, dist, finish=pend.finish)
         plan.timing(False)
         dms, dn = plan.timing_query(dom)
         stages = {k: v[0] for k, v in bd.items()}
@@ -740,13 +773,13 @@ def main(argv=None):
     plan = m.native_plan(dev)
 
     gather = dist and not a.no_gather
-    if gather:
-        from dll.distributed import collate_outputs
+    coll = {}
+    pend = Collator(B * world, ("keypoints", "visibilities"), P, coll)
 
     def step(model=m):
         out = model(batch)
         if gather:   # result collation over RCCL: all_gather of the kpt / vis slabs (P known: no host sync)
-            collate_outputs(out, B * world, max_persons=P)
+            pend.start(out)
         return out
 
     n_sub = max(1, min(a.streams, 4, B // 16))
@@ -757,11 +790,12 @@ def main(argv=None):
     with torch.no_grad():
         for _ in range(a.warmup):
             step()
+        pend.finish()
     breakdown = stage_pass(m, plan, batch, 1)
     mfma_stages = ("fpn0", "hm_conv1", "hm_conv2", "hm_conv3")
     dom = max((k for k in breakdown if k in mfma_stages), key=lambda k: breakdown[k][0], default=None)
     plan.timing(True, stage=dom)
-    el, out = run_steps(a.steps, 0, step, dist)
+    el, out = run_steps(a.steps, 0, step, dist, finish=pend.finish)
     plan.timing(False)
     dms, dn = plan.timing_query(dom) if dom else (0.0, 0)
     stages = {k: v[0] for k, v in breakdown.items()}
@@ -797,7 +831,7 @@ def main(argv=None):
                    "model": "MultiPersonKeypointModel (MobileNetV3-Small+FPN, HeatmapHead)",
                    "global_batch": B * world, "height": a.height, "width": a.width, "persons": P,
                    "precision": a.precision, "parallelism": f"dp{world}", "streams_per_gpu": n_sub,
-                   "gather": bool(gather)},
+                   "gather": bool(gather), "gather_pipelined": bool(gather)},
         "gflop_per_image": round(fl["total"] / 1e9, 3),
         "achieved_tflops_total": round(fl["total"] * total_imgs / el / 1e12, 2),
         "roofline": roof,

@@ -46,9 +46,29 @@ def pad_persons(x: torch.Tensor, p: int) -> torch.Tensor:
     return torch.cat([x, pad], dim=1)
 
 
-def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
-    """all_gather a per-image tensor [n_local, ...] sharded by ``shard_range``
-    into [total, ...] on every rank (uneven shards padded then trimmed)."""
+class PendingCollation:
+    """The all_gathers of one collate_outputs(..., async_op=True) call in flight.
+    ``wait()`` completes them (on RCCL: the caller's stream waits for the
+    collective's stream, no host block) and returns the collated dict.  Until
+    then the caller may enqueue more work -- the next batch's forward -- which
+    then overlaps the collective instead of queueing behind it."""
+
+    def __init__(self, items, group):
+        self._items = items          # key -> (work, parts, counts, send buffer kept alive)
+        self._group = group
+        self._done = None
+
+    def wait(self) -> Dict[str, torch.Tensor]:
+        if self._done is None:
+            res = {}
+            for k, (work, parts, counts, _buf) in self._items.items():
+                work.wait()
+                res[k] = torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
+            self._done, self._items = res, None
+        return self._done
+
+
+def _gather_start(local: torch.Tensor, total: int, group, async_op: bool):
     world = dist.get_world_size(group)
     counts = [shard_range(total, world, r) for r in range(world)]
     mx = max(b - a for a, b in counts)
@@ -58,21 +78,32 @@ def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
         buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         buf[: local.size(0)] = local
     parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
+    work = dist.all_gather(parts, buf, group=group, async_op=async_op)
+    return work, parts, counts, buf
+
+
+def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
+    """all_gather a per-image tensor [n_local, ...] sharded by ``shard_range``
+    into [total, ...] on every rank (uneven shards padded then trimmed)."""
+    _work, parts, counts, _buf = _gather_start(local, total, group, False)
     return torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
 
 
 def collate_outputs(out: Dict[str, torch.Tensor], total: int, group=None,
                     keys: Sequence[str] = ("keypoints", "visibilities"),
-                    max_persons: Optional[int] = None) -> Dict[str, torch.Tensor]:
+                    max_persons: Optional[int] = None, async_op: bool = False):
     """Pad this rank's outputs to the global person count and all-gather ``keys``
     (add "heatmap" to collate the [n,P,17,56,56] heatmaps too: 213 KB per
     person).  ``max_persons``: the global padded person count when the caller
     knows it (a sharded [B,P,4] box tensor: P on every rank; the detector:
-    max_persons) -- then no all_reduce and no host synchronisation happen."""
+    max_persons) -- then no all_reduce and no host synchronisation happen.
+    ``async_op``: return a PendingCollation whose ``wait()`` gives the dict
+    (a serving loop collates batch k while batch k + 1 computes)."""
     p = max_persons
     if p is None:
         p = global_max_persons(out["keypoints"].size(1), out["keypoints"].device, group)
+    if async_op:
+        return PendingCollation({k: _gather_start(pad_persons(out[k], p), total, group, True) for k in keys}, group)
     res = {}
     for k in keys:
         res[k] = gather_images(pad_persons(out[k], p), total, group)

@@ -154,3 +154,50 @@ def test_sharded_forward_oracle_gloo():
             torch.testing.assert_close(res[rank][k], ref[k], atol=1e-5, rtol=0)
     assert torch.equal(res[0]["visibilities"], res[1]["visibilities"])
     assert res[0]["visibilities"][4, 0, 0, :, 0].eq(1).all()    # dummy person: visibility class 0
+
+
+def _async_worker(rank, world, store, q):
+    _init(rank, world, store)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "keypoint-detection_amd"))
+        from dll.distributed import collate_outputs, shard_range
+        total = 7
+        a, b = shard_range(total, world, rank)
+        n = b - a
+        outs = []
+        for step in range(3):   # three steps in flight one at a time, as bench.Collator runs them
+            k = (torch.arange(a, b, dtype=torch.float32) + 100 * step).view(n, 1, 1, 1, 1).expand(n, 2, 1, 17, 2)
+            outs.append({"keypoints": k.contiguous(), "box_scores": torch.full((n, 2), float(step))})
+        pend, got = None, []
+        for o in outs:
+            if pend is not None:
+                got.append(pend.wait())
+            pend = collate_outputs(o, total, keys=("keypoints", "box_scores"), max_persons=3, async_op=True)
+        got.append(pend.wait())
+        sync = [collate_outputs(o, total, keys=("keypoints", "box_scores"), max_persons=3) for o in outs]
+        q.put((rank, all(torch.equal(g[k], s[k]) for g, s in zip(got, sync) for k in g),
+               [tuple(g["keypoints"].shape) for g in got], got[2]["keypoints"][:, 0, 0, 0, 0].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collate_outputs_async_gloo():
+    """async_op=True (bench.py's one-step-deep pipelined collation): each
+    step's PendingCollation.wait() equals the synchronous collation, padded
+    to max_persons, every rank's slab in place."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    store = os.path.join(tempfile.mkdtemp(), "store")
+    procs = [ctx.Process(target=_async_worker, args=(r, world, store, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _rank, same, shapes, first in res:
+        assert same
+        assert shapes == [(7, 3, 1, 17, 2)] * 3
+        assert first == [200.0 + i for i in range(7)]
