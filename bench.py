@@ -139,9 +139,9 @@ def parse(argv=None):
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run (entries are "
                          "stamped with the hash of the kernel sources they were measured on)")
     ap.add_argument("--configs", default="auto",
-                    help="labelled BASELINE config objects after the C2 headline: 'auto' = C3,C5 at N=1 and "
+                    help="labelled BASELINE config objects after the C2 headline: 'auto' = C1,C3,C5 at N=1 and "
                          "C4,C5 at N>1 (C4 = the C3 pipeline per rank with RCCL collation); a comma list; 'none'")
-    ap.add_argument("--only", default=None, choices=sorted(PIPELINES),
+    ap.add_argument("--only", default=None, choices=sorted(PIPELINES) + ["C1"],
                     help="run only this config object (profiling passes)")
     ap.add_argument("--c3-only", dest="only", action="store_const", const="C3", help="= --only C3")
     ap.add_argument("--cfg-batch", type=int, default=0, help="images per rank of the config objects (0 = theirs)")
@@ -363,7 +363,7 @@ def main_standin(a, world, rank, dist):
             torch.equal(coll["visibilities"][s:e, :, 0, :, 2], torch.ones(e - s, P, 17))
             for s, e in (shard_range(B * world, world, r) for r in range(world))))
     cfgs = {}
-    for name in config_names(a, world):
+    for name in config_names(a, world, standin=True):
         cfgs[name] = run_pipeline(name, a, torch.device("cpu"), None, world, rank, dist, cpu=False, standin=True)
     if cfgs:
         line["configs"] = cfgs
@@ -692,15 +692,74 @@ def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, stand
     return res
 
 
-def config_names(a, world):
-    """Labelled config objects of this run: N = 1: C3 + C5; N > 1: C4 + C5."""
+def config_names(a, world, standin=False):
+    """Labelled config objects of this run: N = 1: C1 + C3 + C5; N > 1: C4 + C5
+    (C1 is one image's latency on one GPU; not with the CPU stand-in)."""
     if a.only:
         return [a.only]
     if a.configs == "none":
         return []
     if a.configs == "auto":
-        return ["C3", "C5"] if world == 1 else ["C4", "C5"]
-    return [x for x in a.configs.split(",") if x]
+        names = ["C1", "C3", "C5"] if world == 1 else ["C4", "C5"]
+    else:
+        names = [x for x in a.configs.split(",") if x]
+    return [n for n in names if not (standin and n == "C1")]
+
+
+def run_c1(a, dev, cpu=True):
+    """BASELINE C1: scripts/predict.py's forward -- one 256x192 image, one box --
+    as synchronous latency: median (and p90) of 50 forwards after 10 warm-ups,
+    the same forwards replayed as hipGraphs (kpd_plan_set_graphs; outputs
+    checked identical), beside the CPU reference path (the golden-pinned
+    oracle, 3 warm-ups + median of 5) on this host's CPU share."""
+    from dll.configs import ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
+    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=a.precision, streams=1)
+    sd = synthetic_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(dev).eval()
+    img, box = synthetic_images(1, 3, 256, 192, seed=7), synthetic_boxes(1, 1, seed=8)
+    batch = {"image": img.to(dev), "bboxes": box.to(dev)}
+
+    def lat(n=60, skip=10):
+        ts = []
+        with torch.no_grad():
+            for i in range(n):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                o = m(batch)
+                torch.cuda.synchronize()
+                if i >= skip:
+                    ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts, o
+    ts, out = lat()
+    plan = m.native_plan(dev)
+    plan.set_graphs(True)
+    tg, outg = lat()
+    plan.set_graphs(False)
+    res = {"workload": "C1: one 256x192x3 image, one box (scripts/predict.py's forward), synchronous latency",
+           "gpu_latency_ms": round(ts[len(ts) // 2] * 1e3, 4), "gpu_latency_p90_ms": round(ts[int(len(ts) * .9)] * 1e3, 4),
+           "gpu_latency_graph_ms": round(tg[len(tg) // 2] * 1e3, 4),
+           "graph_outputs_identical": all(torch.equal(out[k], outg[k]) for k in ("keypoints", "visibilities", "heatmap")),
+           "forwards": len(ts), "warmup": 10, "precision": a.precision,
+           "value": round(1.0 / ts[len(ts) // 2], 2), "unit": "images/s (1 / median latency)"}
+    if cpu:
+        from oracle import kpd_oracle as O
+        ci = host_cpu_info()
+        ref, rate, proto = cpu_baseline(sd, img, box, ci["threads"])
+        res["cpu_baseline"] = {"value": round(1e3 / rate, 3), "unit": "ms/image (latency)", "cores": ci["threads"],
+                               "kind": "port", "sample": f"the same image and box, oracle/kpd_oracle.py forward, "
+                                                         f"{proto['warmups']} warmups + median of {proto['runs']} runs",
+                               "protocol": proto, "cpu_model": ci["model"]}
+        res["gpu_vs_cpu_latency"] = round(res["cpu_baseline"]["value"] / res["gpu_latency_ms"], 1)
+        res["parity"] = {"max_abs_dkpt": float((out["keypoints"].cpu() - ref["keypoints"]).abs().max()),
+                         "max_abs_dheat": float((out["heatmap"].cpu() - ref["heatmap"]).abs().max()),
+                         "vis_flips": int((out["visibilities"].cpu() != ref["visibilities"]).any(-1).sum())}
+    del m, plan, out, outg
+    torch.cuda.empty_cache()
+    return res
 
 
 def kernel_src_hash():
@@ -751,7 +810,8 @@ def main(argv=None):
         except ValueError:
             pmc = None
     if a.only:
-        res = run_pipeline(a.only, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline)
+        res = (run_c1(a, dev, cpu=not a.no_cpu_baseline) if a.only == "C1" else
+               run_pipeline(a.only, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline))
         if rank == 0:
             print(json.dumps({"configs": {a.only: res}}), flush=True)
         if dist:
@@ -900,7 +960,8 @@ def main(argv=None):
         # headline, on the same ranks
         del m, plan
         torch.cuda.empty_cache()
-        line["configs"] = {n: run_pipeline(n, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline)
+        line["configs"] = {n: (run_c1(a, dev, cpu=not a.no_cpu_baseline) if n == "C1" else
+                               run_pipeline(n, a, dev, pmc, world, rank, dist, cpu=not a.no_cpu_baseline))
                            for n in names}
     if rank == 0:
         print(json.dumps(line), flush=True)
