@@ -172,17 +172,327 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict_
   if (tid == 0) gb[o] = red[0];
 }
 
+// ===================================================================== fast paths (round 5)
+// forward / dgrad at the heatmap convs' 56 x 56 shape (cin 64 | 256 -> cout
+// 256): the split hmconv kernel in its linear mode (three f16 MFMA products
+// of hi / lo operand splits, fp32 accumulation -- the forward heatmap convs'
+// fp32-accurate arithmetic) on the zero-bordered hmconv layout,
+// then an NHWC -> NCHW transpose.  wgrad for any shape: an fp32 MFMA GEMM over
+// zero-padded planes (exact products), per tap, split over image slices that
+// are summed in order.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kHmSide = 56;
+
+// per-image max|x| -> hsc[n * 4] (float bits; hsc zeroed)
+__global__ __launch_bounds__(256) void k6_amax_kernel(const float* __restrict__ x, long per_img,
+                                                      float* __restrict__ hsc) {
+  const float* src = x + (size_t)blockIdx.y * per_img;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < per_img; i += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(src[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f)
+    atomicMax(reinterpret_cast<unsigned*>(hsc + (size_t)blockIdx.y * 4), __float_as_uint(m));
+}
+
+// x [N][C][56][56] fp32 -> the hmconv split layout [N * 3249][C / 32][hi32 | lo32]
+// f16 at interior positions (borders zeroed by the caller), image n scaled by
+// 2^split_exp_of(hsc[n * 4]) -- the scale hmconv_kernel's split mode unscales by
+__global__ __launch_bounds__(256) void k6_to_hm_kernel(const float* __restrict__ x, int C,
+                                                       const float* __restrict__ hsc, _Float16* __restrict__ out) {
+  __shared__ float t[32][65];
+  const int n = blockIdx.z, cg = blockIdx.y, p0 = blockIdx.x * 64, tid = threadIdx.x;
+  const float* src = x + ((size_t)n * C + cg * 32) * (kHmSide * kHmSide);
+  for (int i = tid; i < 32 * 64; i += 256) {
+    const int c = i >> 6, pp = i & 63;
+    t[c][pp] = p0 + pp < kHmSide * kHmSide ? src[(size_t)c * (kHmSide * kHmSide) + p0 + pp] : 0.f;
+  }
+  __syncthreads();
+  const int pp = tid >> 2, c8 = (tid & 3) * 8, p = p0 + pp;
+  if (p >= kHmSide * kHmSide) return;
+  const float sc = ldexpf(1.f, split_exp_of(hsc[(size_t)n * 4]));
+  const int y = p / kHmSide, xx = p - y * kHmSide;
+  f16x8 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = t[c8 + e][pp] * sc;
+    hi[e] = (_Float16)v;
+    lo[e] = (_Float16)(v - (float)hi[e]);
+  }
+  char* dst = reinterpret_cast<char*>(out) + ((size_t)n * kHmRoiPos + (y + 1) * kHmPitch + xx) * ((size_t)C * 4) +
+              cg * 128 + c8 * 2;
+  *reinterpret_cast<f16x8*>(dst) = hi;
+  *reinterpret_cast<f16x8*>(dst + 64) = lo;
+}
+
+__global__ __launch_bounds__(256) void k6_max_kernel(const float* __restrict__ w, long n, float* __restrict__ out) {
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(w[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
+}
+
+// w [O][C][3][3] -> split weights [co'][9][ci'] as [hi32 | lo32] groups scaled
+// 2^w_exp (pack_split_hm's layout); flip: the dgrad conv's weights, co' = c,
+// ci' = o, tap t <- 8 - t (d(8 - t) = -d(t))
+__global__ __launch_bounds__(256) void k6_pack_w_kernel(const float* __restrict__ w, int O, int C, int flip, int w_exp,
+                                                        _Float16* __restrict__ ws) {
+  const int cin = flip ? O : C, cout = flip ? C : O;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)cout * 9 * cin) return;
+  const int ci = (int)(i % cin);
+  const long r = i / cin;
+  const int t = (int)(r % 9), co = (int)(r / 9);
+  const float v = flip ? w[((size_t)ci * C + co) * 9 + (8 - t)] : w[((size_t)co * C + ci) * 9 + t];
+  const float xs = ldexpf(v, w_exp);
+  const _Float16 hi = (_Float16)xs, lo = (_Float16)(xs - (float)hi);
+  const size_t o = (size_t)r * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
+  ws[o] = hi;
+  ws[o + 32] = lo;
+}
+
+// [N][3136][O] -> [N][O][3136]
+__global__ __launch_bounds__(256) void k6_nhwc_nchw_kernel(const float* __restrict__ in, int O, float* __restrict__ out) {
+  __shared__ float t[64][65];
+  constexpr int HW = kHmSide * kHmSide;
+  const int n = blockIdx.z, o0 = blockIdx.y * 64, p0 = blockIdx.x * 64, tid = threadIdx.x;
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int pp = i >> 6, oo = i & 63;
+    t[pp][oo] = (p0 + pp < HW && o0 + oo < O) ? in[((size_t)n * HW + p0 + pp) * O + o0 + oo] : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < 64 * 64; i += 256) {
+    const int oo = i >> 6, pp = i & 63;
+    if (p0 + pp < HW && o0 + oo < O) out[((size_t)n * O + o0 + oo) * HW + p0 + pp] = t[pp][oo];
+  }
+}
+
+// in [N][Ch][H][W] -> out [N][Chp][Qs]: pixel (y, x) at (y + 1) (W + 2) + x + 1
+// (out zeroed by the caller: borders, pad planes, the tail to Qs)
+__global__ __launch_bounds__(256) void k6_pad_kernel(const float* __restrict__ in, int Ch, int H, int W, int Chp, int Qs,
+                                                     float* __restrict__ out) {
+  const long row = blockIdx.x;   // (n, ch, y)
+  const int y = (int)(row % H);
+  const long nc = row / H;
+  const int ch = (int)(nc % Ch), n = (int)(nc / Ch);
+  const float* src = in + (size_t)row * W;
+  float* dst = out + ((size_t)n * Chp + ch) * Qs + (size_t)(y + 1) * (W + 2) + 1;
+  for (int x = threadIdx.x; x < W; x += 256) dst[x] = src[x];
+}
+
+// wgrad partials: part[s][o][c][t] = sum over the images of slice s and the
+// padded positions q of gyP[n][o][q] * xP[n][c][q + off(t)] (gyP is zero on
+// the border positions, so the border q add nothing and a shifted read past an
+// image's plane is multiplied by zero; xP carries a guard of W + 3 floats at
+// both ends of the buffer).  128 x 128 tiles per tap, 4 waves of 64 x 64,
+// K-steps of 16 positions: a lane's 16-byte LDS read feeds four MFMAs (its K
+// index 4 g + j in step j, on A and B alike).  Exact fp32 products.
+constexpr int kWgT = 128, kWgK = 16, kWgLd = kWgK + 4;
+__global__ __launch_bounds__(256) void k6_wgrad_kernel(const float* __restrict__ gyP, const float* __restrict__ xP,
+                                                       int N, int Op, int Cp, int O, int C, int W2, int Qs, int ips,
+                                                       float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[2][kWgT][kWgLd];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWgT][kWgLd];
+  const int c0 = blockIdx.x * kWgT, o0 = blockIdx.y * kWgT, t = blockIdx.z % 9, s = blockIdx.z / 9;
+  const int off = (t / 3 - 1) * W2 + (t % 3 - 1);
+  const int n0 = s * ips, n1 = min(N, n0 + ips);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int lrow = tid >> 2, lq = (tid & 3) * 4;   // loader: rows lrow, lrow + 64; positions lq .. lq + 3
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int total = (n1 - n0) * (Qs / kWgK);
+  // running load pointers (row lrow; row lrow + 64 is 64 planes on): K-steps
+  // walk a plane, then jump to the same row of the next image
+  const float* pa = gyP + ((size_t)n0 * Op + o0 + lrow) * Qs + lq;
+  const float* pb = xP + ((size_t)n0 * Cp + c0 + lrow) * Qs + lq + off;
+  const size_t ra64 = (size_t)64 * Qs, ajump = (size_t)(Op - 1) * Qs, bjump = (size_t)(Cp - 1) * Qs;
+  int fq = 0;
+  float4 ra0, ra1, rb0, rb1;
+#define K6_FETCH()                                                                   \
+  do {                                                                               \
+    ra0 = *reinterpret_cast<const float4*>(pa);                                      \
+    ra1 = *reinterpret_cast<const float4*>(pa + ra64);                               \
+    rb0 = make_float4(pb[0], pb[1], pb[2], pb[3]);                                   \
+    rb1 = make_float4(pb[ra64], pb[ra64 + 1], pb[ra64 + 2], pb[ra64 + 3]);           \
+    pa += kWgK;                                                                      \
+    pb += kWgK;                                                                      \
+    if ((fq += kWgK) == Qs) { fq = 0; pa += ajump; pb += bjump; }                    \
+  } while (0)
+#define K6_STASH(b)                                                                  \
+  do {                                                                               \
+    *reinterpret_cast<float4*>(&As[b][lrow][lq]) = ra0;                              \
+    *reinterpret_cast<float4*>(&As[b][lrow + 64][lq]) = ra1;                         \
+    *reinterpret_cast<float4*>(&Bs[b][lrow][lq]) = rb0;                              \
+    *reinterpret_cast<float4*>(&Bs[b][lrow + 64][lq]) = rb1;                         \
+  } while (0)
+  if (total > 0) {
+    K6_FETCH();
+    K6_STASH(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < total; ++st) {
+    const int b = st & 1;
+    if (st + 1 < total) K6_FETCH();
+    float4 a4[4], b4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a4[i] = *reinterpret_cast<const float4*>(&As[b][wm * 64 + i * 16 + r16][4 * g]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b4[j] = *reinterpret_cast<const float4*>(&Bs[b][wn * 64 + j * 16 + r16][4 * g]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i].x, b4[j].x, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i].y, b4[j].y, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i].z, b4[j].z, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i].w, b4[j].w, acc[i][j], 0, 0, 0);
+      }
+    if (st + 1 < total) K6_STASH(b ^ 1);
+    __syncthreads();
+  }
+#undef K6_FETCH
+#undef K6_STASH
+  // lane (g, r16) holds rows 4 g + e (o), column r16 (c) of each fragment
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o0 + wm * 64 + i * 16 + g * 4 + e, c = c0 + wn * 64 + j * 16 + r16;
+        if (o < O && c < C) part[(((size_t)s * O + o) * C + c) * 9 + t] = acc[i][j][e];
+      }
+}
+
 }  // namespace
+
+// split forward / dgrad shape: 56 x 56 maps, cin 64 | 256, cout 256
+static bool k6_split_ok(int N, int cin, int cout, int H, int W) {
+  return H == kHmSide && W == kHmSide && (cin == 64 || cin == 256) && cout == 256 &&
+         (long)N * kHmRoiPos * cin * 4 < (1L << 31);
+}
+
+static bool k6_generic() {   // A/B switch (diagnostic build): the round-3 fp32 kernels for all three
+  static const bool g = kpd_diag_env("KPD_K6_GENERIC") != nullptr;
+  return g;
+}
+
+// the weights' power-of-two scale as pack_split_hm chooses it: max|w| < 2^15
+// after scaling (one 4-byte device -> host copy: the launch argument)
+static hipError_t k6_w_exp(const float* w, long n, float* scratch, hipStream_t st, int* w_exp) {
+  hipError_t e = hipMemsetAsync(scratch, 0, sizeof(float), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, w, n, scratch);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  float mx = 0.f;
+  if ((e = hipMemcpyAsync(&mx, scratch, sizeof(float), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  int ex = 0;
+  if (mx > 0.f) std::frexp(mx, &ex);
+  *w_exp = std::min(std::max(14 - ex, -100), 100);
+  return hipSuccess;
+}
+
+// y [N][cout][56][56] = conv3x3(x [N][cin][56][56], w) (+ b) on the split
+// hmconv path; w already oriented [cout][cin][3][3] unless flip (dgrad: w is
+// the forward's [cin][cout][3][3] and is transposed / tap-reversed here)
+static hipError_t k6_split_conv(const float* x, const float* w, const float* b, int N, int cin, int cout, int flip,
+                                float* y, hipStream_t st) {
+  const size_t hm_bytes = (size_t)N * kHmRoiPos * cin * 4, ws_elems = (size_t)cout * 9 * cin * 2;
+  const size_t nhwc = (size_t)N * kHmSide * kHmSide * cout;
+  char* buf = nullptr;
+  const size_t total = hm_bytes + ws_elems * 2 + nhwc * 4 + (size_t)N * 16 + (size_t)cout * 4 + 256 * 5;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), total, st);
+  if (e != hipSuccess) return e;
+  auto carve = [&](size_t bytes) { char* r = buf; buf += (bytes + 255) / 256 * 256; return r; };
+  char* base = buf;
+  _Float16* hm = reinterpret_cast<_Float16*>(carve(hm_bytes));
+  _Float16* ws = reinterpret_cast<_Float16*>(carve(ws_elems * 2));
+  float* yn = reinterpret_cast<float*>(carve(nhwc * 4));
+  float* hsc = reinterpret_cast<float*>(carve((size_t)N * 16));
+  float* zb = reinterpret_cast<float*>(carve((size_t)cout * 4));
+  float* mx = reinterpret_cast<float*>(carve(4));
+  int w_exp = 0;
+  do {
+    if ((e = hipMemsetAsync(hm, 0, hm_bytes, st)) != hipSuccess) break;
+    if ((e = hipMemsetAsync(hsc, 0, (size_t)N * 16, st)) != hipSuccess) break;
+    if (!b) {
+      if ((e = hipMemsetAsync(zb, 0, (size_t)cout * 4, st)) != hipSuccess) break;
+      b = zb;
+    }
+    const long per_img = (long)cin * kHmSide * kHmSide;
+    hipLaunchKernelGGL(k6_amax_kernel, dim3(64, (unsigned)N), dim3(256), 0, st, x, per_img, hsc);
+    hipLaunchKernelGGL(k6_to_hm_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)(cin / 32), (unsigned)N), dim3(256),
+                       0, st, x, cin, hsc, hm);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = k6_w_exp(w, (long)cin * cout * 9, mx, st, &w_exp)) != hipSuccess) break;
+    const long nw = (long)cout * 9 * cin;
+    hipLaunchKernelGGL(k6_pack_w_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, w, flip ? cin : cout,
+                       flip ? cout : cin, flip, w_exp, ws);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    HmConvArgs h{};
+    h.in = hm; h.wt = ws; h.bias = b; h.outf = yn; h.R = N; h.cin = cin; h.cout = cout;
+    h.split = 1; h.hsc = hsc; h.in_c = 0.f; h.in_s = 1.f; h.in_idx = 0; h.out_idx = -1; h.amax_idx = -1;
+    h.w_exp = w_exp;
+    if ((e = launch_hmconv(h, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(k6_nhwc_nchw_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)((cout + 63) / 64), (unsigned)N),
+                       dim3(256), 0, st, yn, cout, y);
+    e = hipGetLastError();
+  } while (false);
+  const hipError_t ef = hipFreeAsync(base, st);
+  return e != hipSuccess ? e : ef;
+}
+
+// gw [O][C][3][3] on the padded-plane GEMM (any shape)
+static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H, int W, int O, float* gw, hipStream_t st) {
+  const int W2 = W + 2, Qs = ((H + 2) * W2 + kWgK - 1) / kWgK * kWgK, G = W + 3;
+  const int Cp = (C + kWgT - 1) / kWgT * kWgT, Op = (O + kWgT - 1) / kWgT * kWgT;
+  const int tiles = (Cp / kWgT) * (Op / kWgT) * 9;
+  // images per K slice: ~2048 workgroups (4 per CU resident: the waves of the
+  // other workgroups hide a K-step's global-load latency)
+  static const int wg_target = kpd_diag_env("KPD_K6_WG") ? atoi(kpd_diag_env("KPD_K6_WG")) : 2048;   // A/B
+  int ips = std::max(1, (N * tiles + wg_target - 1) / wg_target);
+  ips = std::min(ips, N);
+  const int S = (N + ips - 1) / ips;
+  const size_t xb = ((size_t)N * Cp * Qs + 2 * G) * 4, gb = (size_t)N * Op * Qs * 4, pb = (size_t)S * O * C * 9 * 4;
+  char* buf = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), xb + gb + pb + 768, st);
+  if (e != hipSuccess) return e;
+  char* base = buf;
+  auto carve = [&](size_t bytes) { char* r = buf; buf += (bytes + 255) / 256 * 256; return r; };
+  float* xP = reinterpret_cast<float*>(carve(xb));
+  float* gyP = reinterpret_cast<float*>(carve(gb));
+  float* part = reinterpret_cast<float*>(carve(pb));
+  do {
+    if ((e = hipMemsetAsync(xP, 0, xb, st)) != hipSuccess) break;
+    if ((e = hipMemsetAsync(gyP, 0, gb, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * C * H)), dim3(256), 0, st, x, C, H, W, Cp, Qs, xP + G);
+    hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * O * H)), dim3(256), 0, st, gy, O, H, W, Op, Qs, gyP);
+    hipLaunchKernelGGL(k6_wgrad_kernel, dim3((unsigned)(Cp / kWgT), (unsigned)(Op / kWgT), (unsigned)(9 * S)), dim3(256), 0,
+                       st, gyP, xP + G, N, Op, Cp, O, C, W2, Qs, ips, part);
+    const long n = (long)O * C * 9;
+    hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, gw);
+    e = hipGetLastError();
+  } while (false);
+  const hipError_t ef = hipFreeAsync(base, st);
+  return e != hipSuccess ? e : ef;
+}
 
 hipError_t launch_conv3_forward(const float* x, const float* w, const float* b, int N, int C, int H, int W, int O,
                                 float* y, hipStream_t st) {
   if (N <= 0) return hipSuccess;
+  if (!k6_generic() && k6_split_ok(N, C, O, H, W)) return k6_split_conv(x, w, b, N, C, O, 0, y, st);
   const dim3 grid((unsigned)((H * W + TB - 1) / TB), (unsigned)((O + TB - 1) / TB), (unsigned)N);
   hipLaunchKernelGGL(conv3_gemm_kernel<C3_FWD>, grid, dim3(256), 0, st, x, w, nullptr, b, C, H, W, O, 0, 0, y);
   return hipGetLastError();
 }
 
 size_t conv3_wgrad_slices(int N, int H, int W) {
+  if (!k6_generic()) return 0;   // the fast wgrad allocates its own scratch
   const long K = (long)N * H * W;
   const long ks = 4096;
   return (size_t)((K + ks - 1) / ks);
@@ -192,6 +502,17 @@ hipError_t launch_conv3_backward(const float* x, const float* w, const float* gy
                                  float* gx, float* gw, float* gb, float* wgrad_part, hipStream_t st) {
   if (N <= 0) return hipSuccess;
   const int HW = H * W;
+  const bool generic = k6_generic();
+  if (gx && !generic && k6_split_ok(N, O, C, H, W)) {
+    const hipError_t e = k6_split_conv(gy, w, nullptr, N, O, C, 1, gx, st);
+    if (e != hipSuccess) return e;
+    gx = nullptr;
+  }
+  if (gw && !generic) {
+    const hipError_t e = k6_wgrad(x, gy, N, C, H, W, O, gw, st);
+    if (e != hipSuccess) return e;
+    gw = nullptr;
+  }
   if (gx) {
     const dim3 grid((unsigned)((HW + TB - 1) / TB), (unsigned)((C + TB - 1) / TB), (unsigned)N);
     hipLaunchKernelGGL(conv3_gemm_kernel<C3_DGRAD>, grid, dim3(256), 0, st, nullptr, w, gy, nullptr, C, H, W, O, 0, 0,

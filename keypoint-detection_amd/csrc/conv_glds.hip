@@ -1115,7 +1115,7 @@ template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE, int NA
 constexpr int hmconv_lds_bytes() {
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
   constexpr int RING = NAB * hm_awin<BMH>() * ROWB + SB * BN * ROWB * TPS;
-  constexpr int EPI = EMODE != 0 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
+  constexpr int EPI = EMODE != 0 && EMODE != 3 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
   return RING > EPI ? RING : EPI;
 }
 
@@ -1142,6 +1142,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
   static_assert(NTAP == 9 || (NTAP == 10 && EMODE == 2 && SPLIT && !DB), "tenth tap: KH downsample");
   static_assert(EMODE != 2 || (SPLIT && !DB), "KH epilogue: split, single fragment set");
+  static_assert(EMODE != 3 || SPLIT, "linear fp32 epilogue: split");
   constexpr int WAVES_N = BN / 64, WAVES_M = NW / WAVES_N;
   constexpr int WM = BMH / WAVES_M, FM = WM / 16, FN = 4;
   constexpr int AW = hm_awin<BMH>();
@@ -1643,7 +1644,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
         atomicMax(a1, __float_as_uint(two ? w1 : 0.f));
       }
     }
-  } else if constexpr (EMODE == 0) {
+  } else if constexpr (EMODE == 0 || EMODE == 3) {
     // bias + ReLU through the LDS tile (two 128-column halves): bf16 16-byte
     // row stores, or (SPLIT) the unscaled fp32 value re-split for the next
     // conv: x * 2^a_out(ROI) as f16 hi / lo into the [hi32 | lo32] groups
@@ -1675,7 +1676,16 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
         const float4 x0 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8);
         const float4 x1 = *reinterpret_cast<const float4*>(tile + row * P4 + c8 * 8 + 4);
         float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        if constexpr (SPLIT) {
+        if constexpr (EMODE == 3) {
+          // linear fp32 output (conv3x3 forward / dgrad of K6, conv3_grad.hip):
+          // acc * u + bias at NHWC [R][56][56][cout]
+          const float u = m >= rbound ? us[1] : us[0];
+          float* of = p.outf + ((size_t)r * HMS * HMS + yy * HMS + xx) * p.cout + co;
+          *reinterpret_cast<float4*>(of) = make_float4(fmaf(xv[0], u, bv[0]), fmaf(xv[1], u, bv[1]),
+                                                       fmaf(xv[2], u, bv[2]), fmaf(xv[3], u, bv[3]));
+          *reinterpret_cast<float4*>(of + 4) = make_float4(fmaf(xv[4], u, bv[4]), fmaf(xv[5], u, bv[5]),
+                                                           fmaf(xv[6], u, bv[6]), fmaf(xv[7], u, bv[7]));
+        } else if constexpr (SPLIT) {
           const int q = m >= rbound;
           const float u = q ? us[1] : us[0], sc = q ? os[1] : os[0];
           f16x8 hi, lo;
@@ -1700,7 +1710,7 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
         }
       }
     }
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT && EMODE == 0) {
       if (p.amax_idx >= 0) {   // per-ROI max|out| for the next conv's output scale
         const float w0 = wave_max(mx[0]), w1 = wave_max(mx[1]);
         if (lane == 0) {
@@ -2059,9 +2069,34 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
   return hipSuccess;
 }
 
+// Linear mode (outf set, out / fin / kh_ps null; split): fp32 NHWC output of
+// acc * u + bias, no activation -- the conv3x3 forward and dgrad of K6
+// (conv3_grad.hip) on the heatmap convs' 56 x 56 maps; cin 64 or 256, cout 256.
+static hipError_t launch_hmconv_linear(const HmConvArgs& a0, hipStream_t st) {
+  if (!a0.split || !a0.hsc || a0.in_idx < 0 || a0.in_idx > 3 || !a0.bias || a0.cout != 256 ||
+      (a0.cin != 64 && a0.cin != 256) || (long)a0.R * HPP >= 0x7fffffffL)
+    return hipErrorInvalidValue;
+  HmConvArgs a = a0;
+  const long wt_bytes = (long)a.cout * 9 * a.cin * 4;
+  if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;
+  a.wt_bytes = (int)wt_bytes;
+  a.m_off = 0;
+  a.r0 = 0;
+  a.stagger = 1;
+  a.out_idx = -1;
+  a.amax_idx = -1;
+  a.in_bytes = (int)std::min<long>((long)a.R * HPP * a.cin * 4, kMaxDesc);
+  const long rows = (long)a.R * HPP - HP;
+  const dim3 grid((unsigned)((rows + 223) / 224));
+  if (a.cin == 64) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 64, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 256, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_hmconv(const HmConvArgs& a0, hipStream_t st) {
   if (a0.R <= 0) return hipSuccess;
   if (a0.kh_ps) return launch_hmconv_kh(a0, st);
+  if (a0.outf && !a0.out && !a0.fin_w) return launch_hmconv_linear(a0, st);
   const bool fin = a0.fin_w != nullptr, split = a0.split != 0;
   if (a0.cin % (split ? 32 : 64) || (fin ? a0.cout != 64 : a0.cout % 128) ||
       (fin && (!a0.slot || !a0.heat || !a0.fin_b)) || (!fin && !a0.out) ||

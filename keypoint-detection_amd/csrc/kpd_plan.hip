@@ -2172,7 +2172,7 @@ int kpd_conv3x3_backward(const float* x, const float* w, const float* gy, int N,
     return KPD_OK;
   }
   float* part = nullptr;
-  if (gw) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&part),
+  if (gw && conv3_wgrad_slices(N, H, W)) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&part),
                                  sizeof(float) * conv3_wgrad_slices(N, H, W) * O * C * 9, st));
   const hipError_t e = launch_conv3_backward(x, w, gy, N, C, H, W, O, gx, gw, gb, part, st);
   if (part) HIP_TRY(hipFreeAsync(part, st));

@@ -7,8 +7,11 @@ heatmap_head.py:55-66; the gradients autograd computes in Trainer.train,
 trainer.py:263,272).  One JSON line:
 
   per pass: mean ms (HIP events, after warm-ups), algorithmic TFLOP/s
-  (2 * N * HW * O * 9C per pass) and the fraction of the 157.3 TF/s dense fp32
-  MFMA peak the kernels issue on (v_mfma_f32_16x16x4_f32); beside it the same
+  (2 * N * HW * O * 9C per pass) and its fraction of the dense MFMA peak of
+  the dtype the pass issues on: forward / dgrad at 56 x 56 with 64 | 256 -> 256
+  channels run split (3 f16 products per MAC on v_mfma_f32_16x16x32_f16 over
+  the 57 x 57 bordered layout; 2.5 PF/s, the issued rate beside it), the
+  others fp32 (v_mfma_f32_16x16x4_f32; 157.3 TF/s); beside it the same
   passes through torch's own conv (F.conv2d + autograd on this GPU, MIOpen),
   and max |d| of the native gradients vs torch fp64 on a slice.
 
@@ -26,6 +29,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "keypoint-detection_amd"))
 
 PEAK_FP32 = 157.3
+PEAK_F16 = 2500.0
 
 
 def timed(fn, iters, warm=3):
@@ -59,20 +63,30 @@ def main():
     flop = 2.0 * N * H * W * O * 9 * C
 
     res = {"shape": {"rois": N, "cin": C, "cout": O, "h": H, "w": W}, "flop_per_pass": flop,
-           "peak_tflops": PEAK_FP32, "peak_note": "dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md"}
+           "peak_tflops": {"fp32": PEAK_FP32, "f16": PEAK_F16}, "peak_note": "dense MFMA peaks, MI355X_MICROARCH.md"}
     nat = {
         "forward": lambda: _native.conv3x3_forward(x, w, b),
         "dgrad": lambda: _native.conv3x3_backward(x, w, gy, need_x=True, need_w=False, need_b=False),
         "wgrad": lambda: _native.conv3x3_backward(x, w, gy, need_x=False, need_w=True, need_b=False),
         "bias_grad": lambda: _native.conv3x3_backward(x, w, gy, need_x=False, need_w=False, need_b=True),
     }
+    import os
+    generic = bool(os.environ.get("KPD_K6_GENERIC")) and bool(os.environ.get("KPD_DIAG_LIB"))
+    split = {"forward": H == W == 56 and C in (64, 256) and O == 256,
+             "dgrad": H == W == 56 and O in (64, 256) and C == 256}
     for k, fn in nat.items():
         ms = timed(fn, a.iters)
         e = {"ms": round(ms, 4)}
         if k != "bias_grad":
             tf = flop / (ms * 1e-3) / 1e12
-            e.update(tflops=round(tf, 2), frac=round(tf / PEAK_FP32, 4))
+            if split.get(k) and not generic:
+                e.update(tflops=round(tf, 2), path="split_f16x3", frac=round(tf / PEAK_F16, 4),
+                         issued_tflops=round(3 * tf * 57 * 57 / (56 * 56), 2),
+                         issued_frac=round(3 * tf * 57 * 57 / (56 * 56) / PEAK_F16, 4))
+            else:
+                e.update(tflops=round(tf, 2), path="fp32", frac=round(tf / PEAK_FP32, 4))
         res[f"native_{k}"] = e
+    res["native_forward_plus_backward_ms"] = round(sum(res[f"native_{k}"]["ms"] for k in nat), 4)
     # torch's own conv on this GPU (MIOpen) for the same passes
     xr, wr, br = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
 
@@ -95,6 +109,7 @@ def main():
     gx64, gw64, gb64 = torch.autograd.grad(y64, (x64, w64, b64), gy[:n2].double())
     y = _native.conv3x3_forward(x[:n2], w, b)
     gx, gw, gb = _native.conv3x3_backward(x[:n2], w, gy[:n2], need_x=True, need_w=True, need_b=True)
+    y64, gx64, gw64, gb64 = (t.detach() for t in (y64, gx64, gw64, gb64))
     res["max_abs_d_vs_fp64"] = {"y": float((y.double() - y64).abs().max()), "gx": float((gx.double() - gx64).abs().max()),
                                 "gw": float((gw.double() - gw64).abs().max()), "gb": float((gb.double() - gb64).abs().max()),
                                 "images": n2}
