@@ -181,6 +181,7 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict_
 // zero-padded planes (exact products), per tap, split over image slices that
 // are summed in order.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int kHmSide = 56;
 
 // per-image max|x| -> hsc[n * 4] (float bits; hsc zeroed)
@@ -368,6 +369,115 @@ __global__ __launch_bounds__(256) void k6_wgrad_kernel(const float* __restrict__
       }
 }
 
+// wgrad partials on split f16 products: the same GEMM as k6_wgrad_kernel with
+// the operands scaled by powers of two (2^a on gy, 2^b on x, a / b from the
+// tensors' max |.|: split_exp_of) and split into f16 hi + lo while they are
+// staged (fp32 loads, as above), three v_mfma_f32_16x16x32_f16 products per
+// fragment pair (lo.hi, hi.hi, hi.lo: the heatmap convs' fp32-accurate
+// split), fp32 accumulation, unscaled by 2^-(a + b) at the
+// store.  K-steps of 32 positions; an LDS row = [hi 32 | lo 32] f16 + 16 B pad
+// (conflict-free b128 fragment reads).
+constexpr int kWsK = 32, kWsRow = 144;
+__global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __restrict__ gyP, const float* __restrict__ xP,
+                                                             const float* __restrict__ amax, int N, int Op, int Cp,
+                                                             int O, int C, int W2, int Qs, int ips,
+                                                             float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char As[2][kWgT * kWsRow];
+  __shared__ __attribute__((aligned(16))) char Bs[2][kWgT * kWsRow];
+  const int c0 = blockIdx.x * kWgT, o0 = blockIdx.y * kWgT, t = blockIdx.z % 9, s = blockIdx.z / 9;
+  const int off = (t / 3 - 1) * W2 + (t % 3 - 1);
+  const int n0 = s * ips, n1 = min(N, n0 + ips);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int lrow = tid >> 3, lq = (tid & 7) * 4;   // loader: rows lrow + 32 u; positions lq .. lq + 3
+  const int ea = split_exp_of(amax[0]), eb = split_exp_of(amax[1]);
+  const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb), us = ldexpf(1.f, -(ea + eb));
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int total = (n1 - n0) * (Qs / kWsK);
+  const float* pa = gyP + ((size_t)n0 * Op + o0 + lrow) * Qs + lq;
+  const float* pb = xP + ((size_t)n0 * Cp + c0 + lrow) * Qs + lq + off;
+  const size_t r32 = (size_t)32 * Qs, ajump = (size_t)(Op - 1) * Qs, bjump = (size_t)(Cp - 1) * Qs;
+  int fq = 0;
+  float4 ra[4], rb[4];
+#define K6S_FETCH()                                                                                   \
+  do {                                                                                                \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                   \
+      ra[u] = *reinterpret_cast<const float4*>(pa + u * r32);                                         \
+      const float* q = pb + u * r32;                                                                  \
+      rb[u] = make_float4(q[0], q[1], q[2], q[3]);                                                    \
+    }                                                                                                 \
+    pa += kWsK;                                                                                       \
+    pb += kWsK;                                                                                       \
+    if ((fq += kWsK) == Qs) { fq = 0; pa += ajump; pb += bjump; }                                     \
+  } while (0)
+#define K6S_PUT(dst, v, sc)                                                                           \
+  do {                                                                                                \
+    const float e4[4] = {(v).x * (sc), (v).y * (sc), (v).z * (sc), (v).w * (sc)};                     \
+    f16x4 hi, lo;                                                                                     \
+    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                   \
+      hi[e] = (_Float16)e4[e];                                                                        \
+      lo[e] = (_Float16)(e4[e] - (float)hi[e]);                                                       \
+    }                                                                                                 \
+    *reinterpret_cast<f16x4*>(dst) = hi;                                                              \
+    *reinterpret_cast<f16x4*>((dst) + 64) = lo;                                                       \
+  } while (0)
+#define K6S_STASH(b)                                                                                  \
+  do {                                                                                                \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                   \
+      K6S_PUT(&As[b][(lrow + 32 * u) * kWsRow + lq * 2], ra[u], sa);                                  \
+      K6S_PUT(&Bs[b][(lrow + 32 * u) * kWsRow + lq * 2], rb[u], sb);                                  \
+    }                                                                                                 \
+  } while (0)
+  if (total > 0) {
+    K6S_FETCH();
+    K6S_STASH(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < total; ++st) {
+    const int b = st & 1;
+    if (st + 1 < total) K6S_FETCH();
+    f16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const char* q = &As[b][(wm * 64 + i * 16 + r16) * kWsRow + g * 16];
+      ah[i] = *reinterpret_cast<const f16x8*>(q);
+      al[i] = *reinterpret_cast<const f16x8*>(q + 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const char* q = &Bs[b][(wn * 64 + j * 16 + r16) * kWsRow + g * 16];
+      bh[j] = *reinterpret_cast<const f16x8*>(q);
+      bl[j] = *reinterpret_cast<const f16x8*>(q + 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      }
+    if (st + 1 < total) K6S_STASH(b ^ 1);
+    __syncthreads();
+  }
+#undef K6S_FETCH
+#undef K6S_PUT
+#undef K6S_STASH
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o = o0 + wm * 64 + i * 16 + g * 4 + e, c = c0 + wn * 64 + j * 16 + r16;
+        if (o < O && c < C) part[(((size_t)s * O + o) * C + c) * 9 + t] = acc[i][j][e] * us;
+      }
+}
+
 }  // namespace
 
 // split forward / dgrad shape: 56 x 56 maps, cin 64 | 256, cout 256
@@ -449,31 +559,53 @@ static hipError_t k6_split_conv(const float* x, const float* w, const float* b, 
 
 // gw [O][C][3][3] on the padded-plane GEMM (any shape)
 static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H, int W, int O, float* gw, hipStream_t st) {
-  const int W2 = W + 2, Qs = ((H + 2) * W2 + kWgK - 1) / kWgK * kWgK, G = W + 3;
+  // split f16 products (default) or exact fp32 products (KPD_K6_WG32, diagnostic A/B)
+  static const bool fp32 = kpd_diag_env("KPD_K6_WG32") != nullptr;
+  const int W2 = W + 2, Qs = ((H + 2) * W2 + kWsK - 1) / kWsK * kWsK, G = W + 3;
   const int Cp = (C + kWgT - 1) / kWgT * kWgT, Op = (O + kWgT - 1) / kWgT * kWgT;
   const int tiles = (Cp / kWgT) * (Op / kWgT) * 9;
-  // images per K slice: ~2048 workgroups (4 per CU resident: the waves of the
-  // other workgroups hide a K-step's global-load latency)
-  static const int wg_target = kpd_diag_env("KPD_K6_WG") ? atoi(kpd_diag_env("KPD_K6_WG")) : 2048;   // A/B
-  int ips = std::max(1, (N * tiles + wg_target - 1) / wg_target);
-  ips = std::min(ips, N);
+  // images per K slice: the fewest-rounds x longest-slice product over the
+  // resident slots (split: 72 KB of LDS, 2 workgroups per CU; fp32: 4)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const long slots = (long)ncu * (fp32 ? 4 : 2);
+  int ips = N;
+  long best = -1;
+  for (int i = 1; i <= N; ++i) {
+    const long S = (N + i - 1) / i, cost = ((S * tiles + slots - 1) / slots) * i;
+    if (best < 0 || cost < best) { best = cost; ips = i; }
+  }
   const int S = (N + ips - 1) / ips;
   const size_t xb = ((size_t)N * Cp * Qs + 2 * G) * 4, gb = (size_t)N * Op * Qs * 4, pb = (size_t)S * O * C * 9 * 4;
   char* buf = nullptr;
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), xb + gb + pb + 768, st);
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), xb + gb + pb + 1024, st);
   if (e != hipSuccess) return e;
   char* base = buf;
   auto carve = [&](size_t bytes) { char* r = buf; buf += (bytes + 255) / 256 * 256; return r; };
   float* xP = reinterpret_cast<float*>(carve(xb));
   float* gyP = reinterpret_cast<float*>(carve(gb));
   float* part = reinterpret_cast<float*>(carve(pb));
+  float* mx = reinterpret_cast<float*>(carve(8));
   do {
     if ((e = hipMemsetAsync(xP, 0, xb, st)) != hipSuccess) break;
     if ((e = hipMemsetAsync(gyP, 0, gb, st)) != hipSuccess) break;
     hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * C * H)), dim3(256), 0, st, x, C, H, W, Cp, Qs, xP + G);
     hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * O * H)), dim3(256), 0, st, gy, O, H, W, Op, Qs, gyP);
-    hipLaunchKernelGGL(k6_wgrad_kernel, dim3((unsigned)(Cp / kWgT), (unsigned)(Op / kWgT), (unsigned)(9 * S)), dim3(256), 0,
-                       st, gyP, xP + G, N, Op, Cp, O, C, W2, Qs, ips, part);
+    const dim3 grid((unsigned)(Cp / kWgT), (unsigned)(Op / kWgT), (unsigned)(9 * S));
+    if (fp32) {
+      hipLaunchKernelGGL(k6_wgrad_kernel, grid, dim3(256), 0, st, gyP, xP + G, N, Op, Cp, O, C, W2, Qs, ips, part);
+    } else {
+      if ((e = hipMemsetAsync(mx, 0, 8, st)) != hipSuccess) break;
+      hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, gy, (long)N * O * H * W, mx);
+      hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, x, (long)N * C * H * W, mx + 1);
+      hipLaunchKernelGGL(k6_wgrad_split_kernel, grid, dim3(256), 0, st, gyP, xP + G, mx, N, Op, Cp, O, C, W2, Qs, ips,
+                         part);
+    }
     const long n = (long)O * C * 9;
     hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, gw);
     e = hipGetLastError();
