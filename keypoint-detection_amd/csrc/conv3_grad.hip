@@ -191,9 +191,22 @@ __global__ __launch_bounds__(256) void k6_amax_kernel(const float* __restrict__ 
   float m = 0.f;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < per_img; i += (long)gridDim.x * 256)
     m = fmaxf(m, fabsf(src[i]));
+  __shared__ float red[4];
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && m > 0.f)
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (threadIdx.x == 0 && m > 0.f)   // one atomic per workgroup (64 per image)
     atomicMax(reinterpret_cast<unsigned*>(hsc + (size_t)blockIdx.y * 4), __float_as_uint(m));
+}
+
+// hsc[n][1] = hsc[n][0] * 2^-w_exp: the bound whose split_exp_of is a + w_exp
+// (a = split_exp_of(max |x_n|), the input scale of k6_to_hm_kernel), so that
+// hmconv_kernel (in_idx 1, w_exp 0) unscales by 2^-(a + w_exp) with the
+// weights' exponent computed on the device (no host round trip)
+__global__ __launch_bounds__(256) void k6_bound_kernel(float* __restrict__ hsc, int N, const float* __restrict__ wmax) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n < N) hsc[(size_t)n * 4 + 1] = ldexpf(hsc[(size_t)n * 4], -split_exp_of(*wmax));
 }
 
 // x [N][C][56][56] fp32 -> the hmconv split layout [N * 3249][C / 32][hi32 | lo32]
@@ -226,6 +239,18 @@ __global__ __launch_bounds__(256) void k6_to_hm_kernel(const float* __restrict__
   *reinterpret_cast<f16x8*>(dst + 64) = lo;
 }
 
+// the hmconv layout's border positions of image n (row 0: 57 positions; the
+// shared zero column 56 of rows 1 .. 56) set to zero; C channels x 4 bytes each
+__global__ __launch_bounds__(256) void k6_hm_border_kernel(_Float16* __restrict__ out, int C) {
+  const int n = blockIdx.x, per = C / 4;   // 16-byte pieces per position
+  uint4* base = reinterpret_cast<uint4*>(out) + (size_t)n * kHmRoiPos * per;
+  for (int i = threadIdx.x; i < (kHmPitch + kHmSide) * per; i += 256) {
+    const int k = i / per, piece = i - k * per;
+    const int pos = k < kHmPitch ? k : (k - kHmPitch + 1) * kHmPitch + kHmSide;
+    base[(size_t)pos * per + piece] = uint4{0u, 0u, 0u, 0u};
+  }
+}
+
 __global__ __launch_bounds__(256) void k6_max_kernel(const float* __restrict__ w, long n, float* __restrict__ out) {
   float m = 0.f;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(w[i]));
@@ -234,17 +259,20 @@ __global__ __launch_bounds__(256) void k6_max_kernel(const float* __restrict__ w
 }
 
 // w [O][C][3][3] -> split weights [co'][9][ci'] as [hi32 | lo32] groups scaled
-// 2^w_exp (pack_split_hm's layout); flip: the dgrad conv's weights, co' = c,
+// 2^w_exp, w_exp = split_exp_of(max |w|) (pack_split_hm's layout), rows
+// co' >= cout zero up to cout_p; flip: the dgrad conv's weights, co' = c,
 // ci' = o, tap t <- 8 - t (d(8 - t) = -d(t))
-__global__ __launch_bounds__(256) void k6_pack_w_kernel(const float* __restrict__ w, int O, int C, int flip, int w_exp,
+__global__ __launch_bounds__(256) void k6_pack_w_kernel(const float* __restrict__ w, int O, int C, int flip,
+                                                        const float* __restrict__ wmax, int cout_p,
                                                         _Float16* __restrict__ ws) {
+  const int w_exp = split_exp_of(*wmax);
   const int cin = flip ? O : C, cout = flip ? C : O;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)cout * 9 * cin) return;
+  if (i >= (long)cout_p * 9 * cin) return;
   const int ci = (int)(i % cin);
   const long r = i / cin;
   const int t = (int)(r % 9), co = (int)(r / 9);
-  const float v = flip ? w[((size_t)ci * C + co) * 9 + (8 - t)] : w[((size_t)co * C + ci) * 9 + t];
+  const float v = co >= cout ? 0.f : flip ? w[((size_t)ci * C + co) * 9 + (8 - t)] : w[((size_t)co * C + ci) * 9 + t];
   const float xs = ldexpf(v, w_exp);
   const _Float16 hi = (_Float16)xs, lo = (_Float16)(xs - (float)hi);
   const size_t o = (size_t)r * 2 * cin + (size_t)(ci / 32) * 64 + ci % 32;
@@ -252,14 +280,15 @@ __global__ __launch_bounds__(256) void k6_pack_w_kernel(const float* __restrict_
   ws[o + 32] = lo;
 }
 
-// [N][3136][O] -> [N][O][3136]
-__global__ __launch_bounds__(256) void k6_nhwc_nchw_kernel(const float* __restrict__ in, int O, float* __restrict__ out) {
+// [N][3136][Op] (the first O of Op channels) -> [N][O][3136]
+__global__ __launch_bounds__(256) void k6_nhwc_nchw_kernel(const float* __restrict__ in, int O, int Op,
+                                                           float* __restrict__ out) {
   __shared__ float t[64][65];
   constexpr int HW = kHmSide * kHmSide;
   const int n = blockIdx.z, o0 = blockIdx.y * 64, p0 = blockIdx.x * 64, tid = threadIdx.x;
   for (int i = tid; i < 64 * 64; i += 256) {
     const int pp = i >> 6, oo = i & 63;
-    t[pp][oo] = (p0 + pp < HW && o0 + oo < O) ? in[((size_t)n * HW + p0 + pp) * O + o0 + oo] : 0.f;
+    t[pp][oo] = (p0 + pp < HW && o0 + oo < O) ? in[((size_t)n * HW + p0 + pp) * Op + o0 + oo] : 0.f;
   }
   __syncthreads();
   for (int i = tid; i < 64 * 64; i += 256) {
@@ -268,17 +297,68 @@ __global__ __launch_bounds__(256) void k6_nhwc_nchw_kernel(const float* __restri
   }
 }
 
-// in [N][Ch][H][W] -> out [N][Chp][Qs]: pixel (y, x) at (y + 1) (W + 2) + x + 1
-// (out zeroed by the caller: borders, pad planes, the tail to Qs)
-__global__ __launch_bounds__(256) void k6_pad_kernel(const float* __restrict__ in, int Ch, int H, int W, int Chp, int Qs,
-                                                     float* __restrict__ out) {
-  const long row = blockIdx.x;   // (n, ch, y)
-  const int y = (int)(row % H);
-  const long nc = row / H;
-  const int ch = (int)(nc % Ch), n = (int)(nc / Ch);
-  const float* src = in + (size_t)row * W;
-  float* dst = out + ((size_t)n * Chp + ch) * Qs + (size_t)(y + 1) * (W + 2) + 1;
-  for (int x = threadIdx.x; x < W; x += 256) dst[x] = src[x];
+// in [N][Ch][H][W] -> out [N][Chp][Qs]: pixel (y, x) at (y + 1) (W + 2) + x + 1,
+// zero elsewhere (borders, the tail to Qs, planes ch >= Ch); one workgroup
+// per plane (ch, n), coalesced reads and writes.  Also: the plane's max |in|
+// into amax[n][ch] (amax non-null) and, psum non-null, the
+// plane's sum psum[n][ch] (fixed order: a thread's positions ascending, then
+// an LDS tree) -- the bias gradient's partials.  out null: sums / max only.
+__global__ __launch_bounds__(256) void k6_plane_kernel(const float* __restrict__ in, int Ch, int H, int W, int Chp,
+                                                       int Qs, float* __restrict__ out, float* __restrict__ amax,
+                                                       float* __restrict__ psum) {
+  __shared__ float red[256];
+  const int ch = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, W2 = W + 2;
+  const bool live = ch < Ch;
+  const float* src = in + ((size_t)n * Ch + (live ? ch : 0)) * H * W;
+  float* dst = out ? out + ((size_t)n * Chp + ch) * Qs : nullptr;
+  float m = 0.f, sum = 0.f;
+  for (int q = tid; q < Qs; q += 256) {
+    const int yy = q / W2 - 1, xx = q - (yy + 1) * W2 - 1;
+    float v = 0.f;
+    if (live && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      v = src[yy * W + xx];
+      m = fmaxf(m, fabsf(v));
+      sum += v;
+    }
+    if (dst) dst[q] = v;
+  }
+  if (amax) {   // per-plane max |in| (k6_max_finish_kernel reduces them: no same-address atomics)
+    m = wave_max(m);
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) amax[(size_t)n * Chp + ch] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+  }
+  if (psum && live) {
+    red[tid] = sum;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (tid < h) red[tid] += red[tid + h];
+      __syncthreads();
+    }
+    if (tid == 0) psum[(size_t)n * Ch + ch] = red[0];
+  }
+}
+
+// out[0] = max of m[0 .. n)
+__global__ __launch_bounds__(256) void k6_max_finish_kernel(const float* __restrict__ m, long n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float v = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) v = fmaxf(v, m[i]);
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// gb[o] = sum over n (in order) of psum[n][o]
+__global__ __launch_bounds__(256) void k6_bias_finish_kernel(const float* __restrict__ psum, int N, int O,
+                                                             float* __restrict__ gb) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= O) return;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) s += psum[(size_t)n * O + o];
+  gb[o] = s;
 }
 
 // wgrad partials: part[s][o][c][t] = sum over the images of slice s and the
@@ -377,36 +457,43 @@ __global__ __launch_bounds__(256) void k6_wgrad_kernel(const float* __restrict__
 // split), fp32 accumulation, unscaled by 2^-(a + b) at the
 // store.  K-steps of 32 positions; an LDS row = [hi 32 | lo 32] f16 + 16 B pad
 // (conflict-free b128 fragment reads).
+// NWM x NWN waves of 64 x 16 FJ: tiles of 64 NWM (o) x 16 FJ NWN (c); the
+// larger tiles stage fewer operand bytes per MFMA (256 x 256: half of 128 x
+// 128's)
 constexpr int kWsK = 32, kWsRow = 144;
-__global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __restrict__ gyP, const float* __restrict__ xP,
-                                                             const float* __restrict__ amax, int N, int Op, int Cp,
-                                                             int O, int C, int W2, int Qs, int ips,
-                                                             float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) char As[2][kWgT * kWsRow];
-  __shared__ __attribute__((aligned(16))) char Bs[2][kWgT * kWsRow];
-  const int c0 = blockIdx.x * kWgT, o0 = blockIdx.y * kWgT, t = blockIdx.z % 9, s = blockIdx.z / 9;
+template <int NWM, int NWN, int FJ>
+__global__ __launch_bounds__(64 * NWM * NWN) void k6_wgrad_split_kernel(const float* __restrict__ gyP,
+                                                                        const float* __restrict__ xP,
+                                                                        const float* __restrict__ amax, int N, int Op,
+                                                                        int Cp, int O, int C, int W2, int Qs, int ips,
+                                                                        float* __restrict__ part) {
+  constexpr int NT = 64 * NWM * NWN, TM = 64 * NWM, TN = 16 * FJ * NWN, RP = NT / 8, UA = TM / RP, UBn = TN / RP;
+  __shared__ __attribute__((aligned(16))) char As[2][TM * kWsRow];
+  __shared__ __attribute__((aligned(16))) char Bs[2][TN * kWsRow];
+  const int c0 = blockIdx.x * TN, o0 = blockIdx.y * TM, t = blockIdx.z % 9, s = blockIdx.z / 9;
   const int off = (t / 3 - 1) * W2 + (t % 3 - 1);
   const int n0 = s * ips, n1 = min(N, n0 + ips);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / NWN, wn = wave % NWN;
   const int g = lane >> 4, r16 = lane & 15;
-  const int lrow = tid >> 3, lq = (tid & 7) * 4;   // loader: rows lrow + 32 u; positions lq .. lq + 3
+  const int lrow = tid >> 3, lq = (tid & 7) * 4;   // loader: rows lrow + RP u; positions lq .. lq + 3
   const int ea = split_exp_of(amax[0]), eb = split_exp_of(amax[1]);
   const float sa = ldexpf(1.f, ea), sb = ldexpf(1.f, eb), us = ldexpf(1.f, -(ea + eb));
-  f32x4 acc[4][4];
+  f32x4 acc[4][FJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int total = (n1 - n0) * (Qs / kWsK);
   const float* pa = gyP + ((size_t)n0 * Op + o0 + lrow) * Qs + lq;
   const float* pb = xP + ((size_t)n0 * Cp + c0 + lrow) * Qs + lq + off;
-  const size_t r32 = (size_t)32 * Qs, ajump = (size_t)(Op - 1) * Qs, bjump = (size_t)(Cp - 1) * Qs;
+  const size_t r32 = (size_t)RP * Qs, ajump = (size_t)(Op - 1) * Qs, bjump = (size_t)(Cp - 1) * Qs;
   int fq = 0;
-  float4 ra[4], rb[4];
+  float4 ra[UA], rb[UBn];
 #define K6S_FETCH()                                                                                   \
   do {                                                                                                \
-    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                   \
+    _Pragma("unroll") for (int u = 0; u < UA; ++u)                                                    \
       ra[u] = *reinterpret_cast<const float4*>(pa + u * r32);                                         \
+    _Pragma("unroll") for (int u = 0; u < UBn; ++u) {                                                 \
       const float* q = pb + u * r32;                                                                  \
       rb[u] = make_float4(q[0], q[1], q[2], q[3]);                                                    \
     }                                                                                                 \
@@ -427,10 +514,10 @@ __global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __rest
   } while (0)
 #define K6S_STASH(b)                                                                                  \
   do {                                                                                                \
-    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                   \
-      K6S_PUT(&As[b][(lrow + 32 * u) * kWsRow + lq * 2], ra[u], sa);                                  \
-      K6S_PUT(&Bs[b][(lrow + 32 * u) * kWsRow + lq * 2], rb[u], sb);                                  \
-    }                                                                                                 \
+    _Pragma("unroll") for (int u = 0; u < UA; ++u)                                                    \
+      K6S_PUT(&As[b][(lrow + RP * u) * kWsRow + lq * 2], ra[u], sa);                                  \
+    _Pragma("unroll") for (int u = 0; u < UBn; ++u)                                                   \
+      K6S_PUT(&Bs[b][(lrow + RP * u) * kWsRow + lq * 2], rb[u], sb);                                  \
   } while (0)
   if (total > 0) {
     K6S_FETCH();
@@ -440,7 +527,7 @@ __global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __rest
   for (int st = 0; st < total; ++st) {
     const int b = st & 1;
     if (st + 1 < total) K6S_FETCH();
-    f16x8 ah[4], al[4], bh[4], bl[4];
+    f16x8 ah[4], al[4], bh[FJ], bl[FJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const char* q = &As[b][(wm * 64 + i * 16 + r16) * kWsRow + g * 16];
@@ -448,15 +535,15 @@ __global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __rest
       al[i] = *reinterpret_cast<const f16x8*>(q + 64);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const char* q = &Bs[b][(wn * 64 + j * 16 + r16) * kWsRow + g * 16];
+    for (int j = 0; j < FJ; ++j) {
+      const char* q = &Bs[b][(wn * 16 * FJ + j * 16 + r16) * kWsRow + g * 16];
       bh[j] = *reinterpret_cast<const f16x8*>(q);
       bl[j] = *reinterpret_cast<const f16x8*>(q + 64);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < FJ; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
@@ -470,19 +557,20 @@ __global__ __launch_bounds__(256) void k6_wgrad_split_kernel(const float* __rest
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int o = o0 + wm * 64 + i * 16 + g * 4 + e, c = c0 + wn * 64 + j * 16 + r16;
+        const int o = o0 + wm * 64 + i * 16 + g * 4 + e, c = c0 + wn * 16 * FJ + j * 16 + r16;
         if (o < O && c < C) part[(((size_t)s * O + o) * C + c) * 9 + t] = acc[i][j][e] * us;
       }
 }
 
 }  // namespace
 
-// split forward / dgrad shape: 56 x 56 maps, cin 64 | 256, cout 256
+// split forward / dgrad shape: 56 x 56 maps, cin 64 | 256, cout 64 | 256
+// (64 runs as a 128-column tile with zero weights in columns 64 .. 127)
 static bool k6_split_ok(int N, int cin, int cout, int H, int W) {
-  return H == kHmSide && W == kHmSide && (cin == 64 || cin == 256) && cout == 256 &&
+  return H == kHmSide && W == kHmSide && (cin == 64 || cin == 256) && (cout == 64 || cout == 256) &&
          (long)N * kHmRoiPos * cin * 4 < (1L << 31);
 }
 
@@ -491,31 +579,16 @@ static bool k6_generic() {   // A/B switch (diagnostic build): the round-3 fp32 
   return g;
 }
 
-// the weights' power-of-two scale as pack_split_hm chooses it: max|w| < 2^15
-// after scaling (one 4-byte device -> host copy: the launch argument)
-static hipError_t k6_w_exp(const float* w, long n, float* scratch, hipStream_t st, int* w_exp) {
-  hipError_t e = hipMemsetAsync(scratch, 0, sizeof(float), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, w, n, scratch);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  float mx = 0.f;
-  if ((e = hipMemcpyAsync(&mx, scratch, sizeof(float), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-  int ex = 0;
-  if (mx > 0.f) std::frexp(mx, &ex);
-  *w_exp = std::min(std::max(14 - ex, -100), 100);
-  return hipSuccess;
-}
-
 // y [N][cout][56][56] = conv3x3(x [N][cin][56][56], w) (+ b) on the split
 // hmconv path; w already oriented [cout][cin][3][3] unless flip (dgrad: w is
 // the forward's [cin][cout][3][3] and is transposed / tap-reversed here)
 static hipError_t k6_split_conv(const float* x, const float* w, const float* b, int N, int cin, int cout, int flip,
                                 float* y, hipStream_t st) {
-  const size_t hm_bytes = (size_t)N * kHmRoiPos * cin * 4, ws_elems = (size_t)cout * 9 * cin * 2;
-  const size_t nhwc = (size_t)N * kHmSide * kHmSide * cout;
+  const int cout_p = cout == 64 ? 128 : cout;
+  const size_t hm_bytes = (size_t)N * kHmRoiPos * cin * 4, ws_elems = (size_t)cout_p * 9 * cin * 2;
+  const size_t nhwc = (size_t)N * kHmSide * kHmSide * cout_p;
   char* buf = nullptr;
-  const size_t total = hm_bytes + ws_elems * 2 + nhwc * 4 + (size_t)N * 16 + (size_t)cout * 4 + 256 * 5;
+  const size_t total = hm_bytes + ws_elems * 2 + nhwc * 4 + (size_t)N * 16 + (size_t)cout_p * 4 + 256 * 5;
   hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), total, st);
   if (e != hipSuccess) return e;
   auto carve = [&](size_t bytes) { char* r = buf; buf += (bytes + 255) / 256 * 256; return r; };
@@ -524,14 +597,14 @@ static hipError_t k6_split_conv(const float* x, const float* w, const float* b, 
   _Float16* ws = reinterpret_cast<_Float16*>(carve(ws_elems * 2));
   float* yn = reinterpret_cast<float*>(carve(nhwc * 4));
   float* hsc = reinterpret_cast<float*>(carve((size_t)N * 16));
-  float* zb = reinterpret_cast<float*>(carve((size_t)cout * 4));
+  float* zb = reinterpret_cast<float*>(carve((size_t)cout_p * 4));
   float* mx = reinterpret_cast<float*>(carve(4));
-  int w_exp = 0;
   do {
-    if ((e = hipMemsetAsync(hm, 0, hm_bytes, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(k6_hm_border_kernel, dim3((unsigned)N), dim3(256), 0, st, hm, cin);
     if ((e = hipMemsetAsync(hsc, 0, (size_t)N * 16, st)) != hipSuccess) break;
-    if (!b) {
-      if ((e = hipMemsetAsync(zb, 0, (size_t)cout * 4, st)) != hipSuccess) break;
+    if (!b || cout_p != cout) {   // the bias padded to the tile's columns (zero for dgrad)
+      if ((e = hipMemsetAsync(zb, 0, (size_t)cout_p * 4, st)) != hipSuccess) break;
+      if (b && (e = hipMemcpyAsync(zb, b, (size_t)cout * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) break;
       b = zb;
     }
     const long per_img = (long)cin * kHmSide * kHmSide;
@@ -539,31 +612,38 @@ static hipError_t k6_split_conv(const float* x, const float* w, const float* b, 
     hipLaunchKernelGGL(k6_to_hm_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)(cin / 32), (unsigned)N), dim3(256),
                        0, st, x, cin, hsc, hm);
     if ((e = hipGetLastError()) != hipSuccess) break;
-    if ((e = k6_w_exp(w, (long)cin * cout * 9, mx, st, &w_exp)) != hipSuccess) break;
-    const long nw = (long)cout * 9 * cin;
+    if ((e = hipMemsetAsync(mx, 0, sizeof(float), st)) != hipSuccess) break;
+    hipLaunchKernelGGL(k6_max_kernel, dim3(64), dim3(256), 0, st, w, (long)cin * cout * 9, mx);
+    hipLaunchKernelGGL(k6_bound_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, hsc, N, mx);
+    const long nw = (long)cout_p * 9 * cin;
     hipLaunchKernelGGL(k6_pack_w_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, w, flip ? cin : cout,
-                       flip ? cout : cin, flip, w_exp, ws);
+                       flip ? cout : cin, flip, mx, cout_p, ws);
     if ((e = hipGetLastError()) != hipSuccess) break;
     HmConvArgs h{};
-    h.in = hm; h.wt = ws; h.bias = b; h.outf = yn; h.R = N; h.cin = cin; h.cout = cout;
-    h.split = 1; h.hsc = hsc; h.in_c = 0.f; h.in_s = 1.f; h.in_idx = 0; h.out_idx = -1; h.amax_idx = -1;
-    h.w_exp = w_exp;
+    h.in = hm; h.wt = ws; h.bias = b; h.outf = yn; h.R = N; h.cin = cin; h.cout = cout_p;
+    h.split = 1; h.hsc = hsc; h.in_c = 0.f; h.in_s = 1.f; h.in_idx = 1; h.out_idx = -1; h.amax_idx = -1;
+    h.w_exp = 0;
     if ((e = launch_hmconv(h, st)) != hipSuccess) break;
     hipLaunchKernelGGL(k6_nhwc_nchw_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)((cout + 63) / 64), (unsigned)N),
-                       dim3(256), 0, st, yn, cout, y);
+                       dim3(256), 0, st, yn, cout, cout_p, y);
     e = hipGetLastError();
   } while (false);
   const hipError_t ef = hipFreeAsync(base, st);
   return e != hipSuccess ? e : ef;
 }
 
-// gw [O][C][3][3] on the padded-plane GEMM (any shape)
-static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H, int W, int O, float* gw, hipStream_t st) {
+// gw [O][C][3][3] (and gb [O] when non-null, from the gy plane pass) on the
+// padded-plane GEMM (any shape)
+static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H, int W, int O, float* gw, float* gb,
+                           hipStream_t st) {
   // split f16 products (default) or exact fp32 products (KPD_K6_WG32, diagnostic A/B)
   static const bool fp32 = kpd_diag_env("KPD_K6_WG32") != nullptr;
   const int W2 = W + 2, Qs = ((H + 2) * W2 + kWsK - 1) / kWsK * kWsK, G = W + 3;
-  const int Cp = (C + kWgT - 1) / kWgT * kWgT, Op = (O + kWgT - 1) / kWgT * kWgT;
-  const int tiles = (Cp / kWgT) * (Op / kWgT) * 9;
+  // split tiles: 256 rows / columns where the channel count exceeds 128
+  // (conv 2: one 256 x 256 tile per tap), else 128
+  const int TM = (!fp32 && O > kWgT) ? 256 : kWgT, TN = (!fp32 && C > kWgT) ? 256 : kWgT;
+  const int Cp = (C + TN - 1) / TN * TN, Op = (O + TM - 1) / TM * TM;
+  const int tiles = (Cp / TN) * (Op / TM) * 9;
   // images per K slice: the fewest-rounds x longest-slice product over the
   // resident slots (split: 72 KB of LDS, 2 workgroups per CU; fp32: 4)
   static int ncu = 0;
@@ -573,7 +653,7 @@ static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H,
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const long slots = (long)ncu * (fp32 ? 4 : 2);
+  const long slots = (long)ncu * (fp32 ? 4 : TM * TN > kWgT * kWgT ? 1 : 2);   // resident per CU (LDS)
   int ips = N;
   long best = -1;
   for (int i = 1; i <= N; ++i) {
@@ -581,36 +661,61 @@ static hipError_t k6_wgrad(const float* x, const float* gy, int N, int C, int H,
     if (best < 0 || cost < best) { best = cost; ips = i; }
   }
   const int S = (N + ips - 1) / ips;
-  const size_t xb = ((size_t)N * Cp * Qs + 2 * G) * 4, gb = (size_t)N * Op * Qs * 4, pb = (size_t)S * O * C * 9 * 4;
+  const size_t xb = ((size_t)N * Cp * Qs + 2 * G) * 4, gyb = (size_t)N * Op * Qs * 4, pb = (size_t)S * O * C * 9 * 4;
+  const size_t sb = gb ? (size_t)N * O * 4 : 0, mb = (size_t)N * (Cp + Op) * 4;
   char* buf = nullptr;
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), xb + gb + pb + 1024, st);
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&buf), xb + gyb + pb + sb + mb + 1536, st);
   if (e != hipSuccess) return e;
   char* base = buf;
   auto carve = [&](size_t bytes) { char* r = buf; buf += (bytes + 255) / 256 * 256; return r; };
   float* xP = reinterpret_cast<float*>(carve(xb));
-  float* gyP = reinterpret_cast<float*>(carve(gb));
+  float* gyP = reinterpret_cast<float*>(carve(gyb));
   float* part = reinterpret_cast<float*>(carve(pb));
   float* mx = reinterpret_cast<float*>(carve(8));
+  float* psum = gb ? reinterpret_cast<float*>(carve(sb)) : nullptr;
+  float* pmx = reinterpret_cast<float*>(carve(mb));   // per-plane max |.|: x planes, then gy planes
   do {
-    if ((e = hipMemsetAsync(xP, 0, xb, st)) != hipSuccess) break;
-    if ((e = hipMemsetAsync(gyP, 0, gb, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * C * H)), dim3(256), 0, st, x, C, H, W, Cp, Qs, xP + G);
-    hipLaunchKernelGGL(k6_pad_kernel, dim3((unsigned)((long)N * O * H)), dim3(256), 0, st, gy, O, H, W, Op, Qs, gyP);
-    const dim3 grid((unsigned)(Cp / kWgT), (unsigned)(Op / kWgT), (unsigned)(9 * S));
+    // the guards at both ends of xP; max |gy|, max |x| from the plane passes
+    if ((e = hipMemsetAsync(xP, 0, (size_t)G * 4, st)) != hipSuccess) break;
+    if ((e = hipMemsetAsync(xP + G + (size_t)N * Cp * Qs, 0, (size_t)G * 4, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(k6_plane_kernel, dim3((unsigned)Cp, (unsigned)N), dim3(256), 0, st, x, C, H, W, Cp, Qs, xP + G,
+                       pmx, nullptr);
+    hipLaunchKernelGGL(k6_plane_kernel, dim3((unsigned)Op, (unsigned)N), dim3(256), 0, st, gy, O, H, W, Op, Qs, gyP,
+                       pmx + (size_t)N * Cp, psum);
+    hipLaunchKernelGGL(k6_max_finish_kernel, dim3(1), dim3(256), 0, st, pmx + (size_t)N * Cp, (long)N * Op, mx);
+    hipLaunchKernelGGL(k6_max_finish_kernel, dim3(1), dim3(256), 0, st, pmx, (long)N * Cp, mx + 1);
+    if (gb) hipLaunchKernelGGL(k6_bias_finish_kernel, dim3((unsigned)((O + 255) / 256)), dim3(256), 0, st, psum, N, O, gb);
+    const dim3 grid((unsigned)(Cp / TN), (unsigned)(Op / TM), (unsigned)(9 * S));
     if (fp32) {
       hipLaunchKernelGGL(k6_wgrad_kernel, grid, dim3(256), 0, st, gyP, xP + G, N, Op, Cp, O, C, W2, Qs, ips, part);
     } else {
-      if ((e = hipMemsetAsync(mx, 0, 8, st)) != hipSuccess) break;
-      hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, gy, (long)N * O * H * W, mx);
-      hipLaunchKernelGGL(k6_max_kernel, dim3(256), dim3(256), 0, st, x, (long)N * C * H * W, mx + 1);
-      hipLaunchKernelGGL(k6_wgrad_split_kernel, grid, dim3(256), 0, st, gyP, xP + G, mx, N, Op, Cp, O, C, W2, Qs, ips,
-                         part);
+#define K6S_LAUNCH(M_, N_, F_)                                                                              \
+  hipLaunchKernelGGL((k6_wgrad_split_kernel<M_, N_, F_>), grid, dim3(64 * M_ * N_), 0, st, gyP, xP + G, mx, N, Op, \
+                     Cp, O, C, W2, Qs, ips, part)
+      if (TM == 256 && TN == 256) K6S_LAUNCH(4, 2, 8);
+      else if (TM == 256) K6S_LAUNCH(4, 2, 4);
+      else if (TN == 256) K6S_LAUNCH(2, 4, 4);
+      else K6S_LAUNCH(2, 2, 4);
+#undef K6S_LAUNCH
     }
     const long n = (long)O * C * 9;
     hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, gw);
     e = hipGetLastError();
   } while (false);
   const hipError_t ef = hipFreeAsync(base, st);
+  return e != hipSuccess ? e : ef;
+}
+
+// gb [O] alone: plane sums of gy, summed over the images in order
+static hipError_t k6_bias(const float* gy, int N, int O, int H, int W, float* gb, hipStream_t st) {
+  float* psum = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&psum), (size_t)N * O * 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k6_plane_kernel, dim3((unsigned)O, (unsigned)N), dim3(256), 0, st, gy, O, H, W, O,
+                     (H + 2) * (W + 2), nullptr, nullptr, psum);
+  hipLaunchKernelGGL(k6_bias_finish_kernel, dim3((unsigned)((O + 255) / 256)), dim3(256), 0, st, psum, N, O, gb);
+  e = hipGetLastError();
+  const hipError_t ef = hipFreeAsync(psum, st);
   return e != hipSuccess ? e : ef;
 }
 
@@ -641,9 +746,14 @@ hipError_t launch_conv3_backward(const float* x, const float* w, const float* gy
     gx = nullptr;
   }
   if (gw && !generic) {
-    const hipError_t e = k6_wgrad(x, gy, N, C, H, W, O, gw, st);
+    const hipError_t e = k6_wgrad(x, gy, N, C, H, W, O, gw, gb, st);
     if (e != hipSuccess) return e;
-    gw = nullptr;
+    gw = gb = nullptr;
+  }
+  if (gb && !generic) {
+    const hipError_t e = k6_bias(gy, N, O, H, W, gb, st);
+    if (e != hipSuccess) return e;
+    gb = nullptr;
   }
   if (gx) {
     const dim3 grid((unsigned)((HW + TB - 1) / TB), (unsigned)((C + TB - 1) / TB), (unsigned)N);

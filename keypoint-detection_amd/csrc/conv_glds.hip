@@ -2071,9 +2071,10 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
 
 // Linear mode (outf set, out / fin / kh_ps null; split): fp32 NHWC output of
 // acc * u + bias, no activation -- the conv3x3 forward and dgrad of K6
-// (conv3_grad.hip) on the heatmap convs' 56 x 56 maps; cin 64 or 256, cout 256.
+// (conv3_grad.hip) on the heatmap convs' 56 x 56 maps; cin 64 or 256, cout 256
+// (or 128: a 64-channel output padded with zero weights).
 static hipError_t launch_hmconv_linear(const HmConvArgs& a0, hipStream_t st) {
-  if (!a0.split || !a0.hsc || a0.in_idx < 0 || a0.in_idx > 3 || !a0.bias || a0.cout != 256 ||
+  if (!a0.split || !a0.hsc || a0.in_idx < 0 || a0.in_idx > 3 || !a0.bias || (a0.cout != 256 && a0.cout != 128) ||
       (a0.cin != 64 && a0.cin != 256) || (long)a0.R * HPP >= 0x7fffffffL)
     return hipErrorInvalidValue;
   HmConvArgs a = a0;
@@ -2087,9 +2088,17 @@ static hipError_t launch_hmconv_linear(const HmConvArgs& a0, hipStream_t st) {
   a.amax_idx = -1;
   a.in_bytes = (int)std::min<long>((long)a.R * HPP * a.cin * 4, kMaxDesc);
   const long rows = (long)a.R * HPP - HP;
-  const dim3 grid((unsigned)((rows + 223) / 224));
-  if (a.cin == 64) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 64, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 256, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+  // cout 256: the heatmap conv 1 / 2 tiles (224 x 256, 2-stage weight ring);
+  // cout 128: 256 x 128 tiles with a 4-stage ring (the split BN = 128 variant)
+  if (a.cout == 256) {
+    const dim3 grid((unsigned)((rows + 223) / 224));
+    if (a.cin == 64) hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 64, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((hmconv_kernel<256, 2, 0, 224, true, 256, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+  } else {
+    const dim3 grid((unsigned)((rows + BM - 1) / BM));
+    if (a.cin == 64) hipLaunchKernelGGL((hmconv_kernel<128, 4, 0, BM, true, 64, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((hmconv_kernel<128, 4, 0, BM, true, 256, 1, false, 8, 3>), grid, dim3(NT), 0, st, a);
+  }
   return hipGetLastError();
 }
 
