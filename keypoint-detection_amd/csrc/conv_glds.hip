@@ -1712,8 +1712,23 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     }
     if constexpr (SPLIT && EMODE == 0) {
       if (p.amax_idx >= 0) {   // per-ROI max|out| for the next conv's output scale
-        const float w0 = wave_max(mx[0]), w1 = wave_max(mx[1]);
+        float w0 = wave_max(mx[0]), w1 = wave_max(mx[1]);
+        // the tile's maxima combined in LDS first: two atomics per tile instead
+        // of two per wave (a round of tiles ends together, and same-address
+        // atomics serialise at the L2)
+        float* red = reinterpret_cast<float*>(lds);
+        __syncthreads();   // every wave's reads of the staged tile are done
         if (lane == 0) {
+          red[2 * wave] = w0;
+          red[2 * wave + 1] = w1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll
+          for (int w = 1; w < NW; ++w) {
+            w0 = fmaxf(w0, red[2 * w]);
+            w1 = fmaxf(w1, red[2 * w + 1]);
+          }
           if (w0 > 0.f)
             atomicMax(reinterpret_cast<unsigned*>(p.hsc + (size_t)(p.r0 + rlo) * 4 + p.amax_idx), __float_as_uint(w0));
           if (w1 > 0.f && rlo + 1 < p.R)
