@@ -765,8 +765,13 @@ struct Stage {
     if (!p->timing || (!p->timing_only.empty() && p->timing_only != name)) return;
     auto& t = p->timers[name];
     if (t.used == t.ev.size()) {
+      // timing-only events: no system-scope fence when they are recorded (the
+      // default event's release writes back / invalidates the L2s, ~6 us a
+      // record on this device, inside the measured interval and in the way of
+      // the next kernel); KPD_EVENT_FENCE=1 (diagnostic build): default events, A/B
+      static const unsigned flags = kpd_diag_env("KPD_EVENT_FENCE") ? hipEventDefault : hipEventDisableSystemFence;
       hipEvent_t a, b;
-      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      if (hipEventCreateWithFlags(&a, flags) != hipSuccess || hipEventCreateWithFlags(&b, flags) != hipSuccess) return;
       t.ev.emplace_back(a, b);
     }
     auto& pr = t.ev[t.used++];
