@@ -169,7 +169,7 @@ def main():
     ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"])
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--configs", default="C1,C3,C5")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r04" / "pmc.json"),
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r05" / "pmc.json"),
                     help="rocprofv3 --pmc summary (tools/prof_stages.py --tag <config>) for roofline.traffic")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
