@@ -7,15 +7,18 @@
 //   dgrad    gx[n][c][p] = sum_{o,t} w[o][c][t] gy[n][o][p - d(t)]
 //   wgrad    gw[o][c][t] = sum_{n,p} gy[n][o][p] x[n][c][p + d(t)]
 //   bias     gb[o]       = sum_{n,p} gy[n][o][p]
-// (t = ky*3 + kx, d(t) = (ky - 1, kx - 1), zero outside the map).  All three
-// are one implicit GEMM kernel on v_mfma_f32_16x16x4_f32 (exact fp32
-// products, fp32 accumulation): 64 x 64 output tiles, K in steps of 16 staged
-// through LDS by coalesced gathers along each operand's contiguous axis, four
-// waves of 2 x 2 fragments.  wgrad splits K (images x pixels) into fixed
-// slices whose partial sums are added in slice order, and the bias sums run
-// in a fixed tree: every result is deterministic.  Training is outside the
-// hot path; these kernels are correctness-first and
-// MFMA-tiled, not tuned.
+// (t = ky*3 + kx, d(t) = (ky - 1, kx - 1), zero outside the map).
+// Default paths (round 5): forward and dgrad at the heatmap
+// convs' 56 x 56 shapes (cin 64 | 256 -> cout 64 | 256) on the split hmconv
+// kernel in its linear epilogue mode (three f16 products per MAC, fp32
+// accumulation: the forward heatmap convs' arithmetic); wgrad (any shape) as
+// a per-tap GEMM over zero-padded planes on the same split products; the bias
+// from per-plane sums.  Fallback for other forward / dgrad shapes, and for all
+// three under KPD_K6_GENERIC (diagnostic build): one implicit GEMM kernel on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products): 64 x 64 output tiles, K in
+// steps of 16 staged through LDS, four waves of 2 x 2 fragments.  wgrad sums
+// fixed K slices in slice order and the bias sums run in fixed orders: every
+// result is deterministic.
 #include <algorithm>
 
 #include "kpd_common.h"
