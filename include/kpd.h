@@ -286,8 +286,11 @@ int kpd_conv1x1(const float* x, int B, int Cin, int HW, const float* w, const fl
 /* Training side (the backward of the heatmap head's 3x3
  * convolutions: nn.Conv2d(C, O, 3, padding=1), heatmap_head.py:31-45,55-66,
  * whose gradients the reference takes from autograd in Trainer.train,
- * trainer.py:263,272).  NCHW fp32 device tensors, exact fp32 products
- * (v_mfma_f32_16x16x4_f32), deterministic fixed-order sums.
+ * trainer.py:263,272).  NCHW fp32 device tensors; fp32-accurate arithmetic
+ * (the heatmap convs' split f16 hi / lo products with fp32 accumulation at
+ * 56 x 56 with 64 | 256 channels, and for every wgrad; exact fp32 products
+ * otherwise), deterministic fixed-order sums.  Scratch comes from the
+ * stream-ordered allocator; no host synchronisation.
  *   kpd_conv3x3_forward:  y [N][O][H][W] = conv(x [N][C][H][W], w [O][C][3][3]) + b (b nullable)
  *   kpd_conv3x3_backward: for gy = dL/dy [N][O][H][W]: gx = dL/dx, gw = dL/dw
  *                         [O][C][3][3], gb = dL/db [O] (each nullable). */
