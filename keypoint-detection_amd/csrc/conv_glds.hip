@@ -1111,11 +1111,19 @@ constexpr int hm_epi_parts() { return BMH > 256 ? 2 : 1; }
 // 1 when the input is a single 128-byte chunk (CIN 32 split: one window per tile)
 template <int CIN, bool SPLIT>
 constexpr int hm_nab() { return (CIN > 0 && (SPLIT ? CIN * 4 : CIN * 2) == 128) ? 1 : 2; }
+// KEYPOINT_HEAD epilogue (MODE 2, BN 128) row parts and staged bytes: the
+// fp32 accumulators of BMH / parts rows x BN columns, plus the downsample's of
+// the first 64 columns
+template <int BMH>
+constexpr int kh_epi_parts() { return BMH > 128 ? 2 : 1; }
+template <int BN, int BMH>
+constexpr int kh_epi_bytes() { return BMH / kh_epi_parts<BMH>() * ((BN + 4) + 68) * 4; }
 template <int BN, int SB, int BMH, bool SPLIT, int TPS, int NW, int MODE, int NAB = 2>
 constexpr int hmconv_lds_bytes() {
   constexpr int EMODE = MODE >= 0 ? MODE : (BN == 64 ? 1 : 0);
   constexpr int RING = NAB * hm_awin<BMH>() * ROWB + SB * BN * ROWB * TPS;
-  constexpr int EPI = EMODE != 0 && EMODE != 3 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
+  constexpr int EPI = EMODE == 2 ? (BN == 128 ? kh_epi_bytes<BN, BMH>() : 0)
+                      : EMODE != 0 && EMODE != 3 ? 0 : epi_lds_bytes<BMH / hm_epi_parts<BMH>(), 128, NW * 64>();
   return RING > EPI ? RING : EPI;
 }
 
@@ -1814,59 +1822,156 @@ __device__ __forceinline__ void hmconv_tile(const HmConvArgs& p, char* lds, cons
     //   NTAP 10: v = relu6(v + downsample * u + bd[co])               (identity branch)
     // columns [0, ns) -> the next conv's split operand (padded map, scale os);
     // [ns, ns + nf) -> fp32 [R][56][56][nf] (adaptive-pool inputs); beyond: padding.
-    // A DPP quad transpose gives each lane 4 consecutive columns of one row.
-    const int t4 = lane & 3, q4 = r16 >> 2;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        quad_transpose(acc[i][j], t4);
-        if constexpr (NTAP == 10) quad_transpose(acc2[i][j], t4);
-      }
-    auto relu6 = [](float x) { return fminf(fmaxf(x, 0.f), 6.f); };
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int co = n0 + wn * 64 + j * 16 + q4 * 4;
-      if (co >= p.ns + p.nf) continue;
-      const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
-      const float4 ps = *reinterpret_cast<const float4*>(p.kh_ps + co);
-      const float4 pt = *reinterpret_cast<const float4*>(p.kh_pt + co);
-      float4 bd = make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (NTAP == 10) bd = *reinterpret_cast<const float4*>(p.kh_bd + co);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, sv[4] = {ps.x, ps.y, ps.z, ps.w}, tv[4] = {pt.x, pt.y, pt.z, pt.w};
-      const float dv[4] = {bd.x, bd.y, bd.z, bd.w};
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * WM + i * 16 + g * 4 + t4;
-        int r, yy, xx;
-        if (!interior(m, r, yy, xx)) continue;
-        const int q = m >= rbound;
-        const float u = q ? us[1] : us[0];
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = relu6(fmaf(acc[i][j][e], u, bv[e]));
-          x = relu6(fmaf(x, sv[e], tv[e]));
-          if constexpr (NTAP == 10) x = relu6(x + fmaf(acc2[i][j][e], u, dv[e]));
-          o[e] = x;
-        }
-        if (co < p.ns) {
-          const float sc = q ? os[1] : os[0];
-          f16x4 hi, lo;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float xs = o[e] * sc;
-            hi[e] = (_Float16)xs;
-            lo[e] = (_Float16)(xs - (float)hi[e]);
+    if constexpr (BN == 128) {
+      // The accumulators go through LDS in row parts (and the downsample's for
+      // the first 64 columns), then a thread takes 8 consecutive columns of a
+      // row: 16-byte stores of whole [hi32 | lo32] pieces / fp32 runs (the
+      // per-fragment 8-byte stores took 16 % of a ResidualBlock-1 tile: 7.2 ->
+      // 5.4 us; the 64-column convs with 16 / 32 live columns keep the
+      // per-fragment stores, which skip the padding fragments)
+      constexpr int KRP = kh_epi_parts<BMH>(), BR = BMH / KRP, WPR = WAVES_M / KRP, P1 = BN + 4, P2 = 68;
+      static_assert(WAVES_M % KRP == 0 && BR % WM == 0, "KEYPOINT_HEAD epilogue row parts");
+      static_assert(kh_epi_bytes<BN, BMH>() <= hmconv_lds_bytes<BN, SB, BMH, SPLIT, TPS, NW, MODE, NAB>(),
+                    "KEYPOINT_HEAD epilogue stage");
+      float* t1 = reinterpret_cast<float*>(lds);
+      float* t2 = t1 + BR * P1;
+      constexpr int C8 = BN / 8, RS = NTH / C8, IT = (BR + RS - 1) / RS;
+      const int c8 = tid % C8, row0 = tid / C8, cl = c8 * 8, co = n0 + cl;
+      const bool live = co < p.ns + p.nf;   // ns % 32 == 0, nf % 16 == 0: a group is all split, all fp32 or padding
+      auto relu6 = [](float x) { return fminf(fmaxf(x, 0.f), 6.f); };
+      float bv[8], sv[8], tv[8], dv[8];
+  #pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = sv[e] = tv[e] = dv[e] = 0.f;
+      if (live) {
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.bias + co + 4 * h);
+          const float4 ps = *reinterpret_cast<const float4*>(p.kh_ps + co + 4 * h);
+          const float4 pt = *reinterpret_cast<const float4*>(p.kh_pt + co + 4 * h);
+          bv[4 * h] = bb.x; bv[4 * h + 1] = bb.y; bv[4 * h + 2] = bb.z; bv[4 * h + 3] = bb.w;
+          sv[4 * h] = ps.x; sv[4 * h + 1] = ps.y; sv[4 * h + 2] = ps.z; sv[4 * h + 3] = ps.w;
+          tv[4 * h] = pt.x; tv[4 * h + 1] = pt.y; tv[4 * h + 2] = pt.z; tv[4 * h + 3] = pt.w;
+          if constexpr (NTAP == 10) {
+            const float4 bd = *reinterpret_cast<const float4*>(p.kh_bd + co + 4 * h);
+            dv[4 * h] = bd.x; dv[4 * h + 1] = bd.y; dv[4 * h + 2] = bd.z; dv[4 * h + 3] = bd.w;
           }
-          char* ob = static_cast<char*>(p.out) + (size_t)m * (p.ns * 4) + (co >> 5) * 128 + (co & 31) * 2;
-          *reinterpret_cast<f16x4*>(ob) = hi;
-          *reinterpret_cast<f16x4*>(ob + 64) = lo;
-        } else {
-          *reinterpret_cast<float4*>(p.outf + ((size_t)r * HMS * HMS + yy * HMS + xx) * p.nf +
-                                     (co - p.ns)) = make_float4(o[0], o[1], o[2], o[3]);
         }
       }
+  #pragma unroll
+      for (int pr = 0; pr < KRP; ++pr) {
+        if (pr) __syncthreads();   // the previous part's reads are done
+        if (wm / WPR == pr) {
+          acc_to_lds<FM, FN, WM, 64, BN>(t1, acc, wm % WPR, wn, lane);
+          if constexpr (NTAP == 10)
+            if (wn == 0) acc_to_lds<FM, FN, WM, 64, 64>(t2, acc2, wm % WPR, 0, lane);
+        }
+        __syncthreads();
+        if (!live) continue;
+  #pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          const int row = row0 + it * RS, m = m0 + pr * BR + row;
+          int r, yy, xx;
+          if (row >= BR || !interior(m, r, yy, xx)) continue;
+          const int q = m >= rbound;
+          const float u = q ? us[1] : us[0];
+          const float4 x0 = *reinterpret_cast<const float4*>(t1 + row * P1 + cl);
+          const float4 x1 = *reinterpret_cast<const float4*>(t1 + row * P1 + cl + 4);
+          const float xa[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          float da[8];
+  #pragma unroll
+          for (int e = 0; e < 8; ++e) da[e] = 0.f;
+          if constexpr (NTAP == 10) {
+            if (cl < 64) {
+              const float4 d0 = *reinterpret_cast<const float4*>(t2 + row * P2 + cl);
+              const float4 d1 = *reinterpret_cast<const float4*>(t2 + row * P2 + cl + 4);
+              da[0] = d0.x; da[1] = d0.y; da[2] = d0.z; da[3] = d0.w;
+              da[4] = d1.x; da[5] = d1.y; da[6] = d1.z; da[7] = d1.w;
+            }
+          }
+          float o[8];
+  #pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x = relu6(fmaf(xa[e], u, bv[e]));
+            x = relu6(fmaf(x, sv[e], tv[e]));
+            if constexpr (NTAP == 10) x = relu6(x + fmaf(da[e], u, dv[e]));
+            o[e] = x;
+          }
+          if (co < p.ns) {
+            const float sc = q ? os[1] : os[0];
+            f16x8 hi, lo;
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float xs = o[e] * sc;
+              hi[e] = (_Float16)xs;
+              lo[e] = (_Float16)(xs - (float)hi[e]);
+            }
+            char* ob = static_cast<char*>(p.out) + (size_t)m * (p.ns * 4) + (co >> 5) * 128 + (co & 31) * 2;
+            *reinterpret_cast<f16x8*>(ob) = hi;
+            *reinterpret_cast<f16x8*>(ob + 64) = lo;
+          } else {
+            float* of = p.outf + ((size_t)r * HMS * HMS + yy * HMS + xx) * p.nf + (co - p.ns);
+            *reinterpret_cast<float4*>(of) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4*>(of + 4) = make_float4(o[4], o[5], o[6], o[7]);
+          }
+        }
+      }
+  
+    } else {
+      // A DPP quad transpose gives each lane 4 consecutive columns of one row.
+      const int t4 = lane & 3, q4 = r16 >> 2;
+  #pragma unroll
+      for (int i = 0; i < FM; ++i)
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          quad_transpose(acc[i][j], t4);
+          if constexpr (NTAP == 10) quad_transpose(acc2[i][j], t4);
+        }
+      auto relu6 = [](float x) { return fminf(fmaxf(x, 0.f), 6.f); };
+  #pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = n0 + wn * 64 + j * 16 + q4 * 4;
+        if (co >= p.ns + p.nf) continue;
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+        const float4 ps = *reinterpret_cast<const float4*>(p.kh_ps + co);
+        const float4 pt = *reinterpret_cast<const float4*>(p.kh_pt + co);
+        float4 bd = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (NTAP == 10) bd = *reinterpret_cast<const float4*>(p.kh_bd + co);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, sv[4] = {ps.x, ps.y, ps.z, ps.w}, tv[4] = {pt.x, pt.y, pt.z, pt.w};
+        const float dv[4] = {bd.x, bd.y, bd.z, bd.w};
+  #pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wm * WM + i * 16 + g * 4 + t4;
+          int r, yy, xx;
+          if (!interior(m, r, yy, xx)) continue;
+          const int q = m >= rbound;
+          const float u = q ? us[1] : us[0];
+          float o[4];
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = relu6(fmaf(acc[i][j][e], u, bv[e]));
+            x = relu6(fmaf(x, sv[e], tv[e]));
+            if constexpr (NTAP == 10) x = relu6(x + fmaf(acc2[i][j][e], u, dv[e]));
+            o[e] = x;
+          }
+          if (co < p.ns) {
+            const float sc = q ? os[1] : os[0];
+            f16x4 hi, lo;
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float xs = o[e] * sc;
+              hi[e] = (_Float16)xs;
+              lo[e] = (_Float16)(xs - (float)hi[e]);
+            }
+            char* ob = static_cast<char*>(p.out) + (size_t)m * (p.ns * 4) + (co >> 5) * 128 + (co & 31) * 2;
+            *reinterpret_cast<f16x4*>(ob) = hi;
+            *reinterpret_cast<f16x4*>(ob + 64) = lo;
+          } else {
+            *reinterpret_cast<float4*>(p.outf + ((size_t)r * HMS * HMS + yy * HMS + xx) * p.nf +
+                                       (co - p.ns)) = make_float4(o[0], o[1], o[2], o[3]);
+          }
+        }
+      }
+  
     }
   }
   if (p.stamps) {
