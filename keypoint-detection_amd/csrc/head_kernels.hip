@@ -449,8 +449,16 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, const float* __restrict__ bound,
                                                      int bdiv, int bstride, float* __restrict__ hsc,
-                                                     _Float16* __restrict__ out) {
+                                                     _Float16* __restrict__ out,
+                                                     unsigned long long* __restrict__ stamps) {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  // KPD_STAMPS (diagnostic): start | first T row | sampled | top-k + stats |
+  // attention | stored (vmcnt drained)
+  auto stamp = [&](int i) {
+    if (stamps && threadIdx.x == 0)
+      stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   __shared__ float red[4][2][TOPK];
   __shared__ float spart[4][64];
   __shared__ float satt[64];
@@ -464,7 +472,8 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
   if (tid == 0 && ph == 0) hsc[(size_t)r * 4 + 2] = bnd;
 
   float acc[NB][2], count;
-  roi_row_sample<2>(feat, Hf, Wf, 2 * TOPK, nullptr, boxes, ph, r, b, stage_cap, stage, acc, &count, nullptr);
+  roi_row_sample<2>(feat, Hf, Wf, 2 * TOPK, nullptr, boxes, ph, r, b, stage_cap, stage, acc, &count, stamps);
+  stamp(2);
   // attention weights (wave w: output channels 16 w .. 16 w + 15), loaded
   // after the sampling (held through it they cost the kernel its occupancy);
   // their latency overlaps the top-k / statistics phase below
@@ -509,6 +518,7 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
     st[lane] = s;
     st[TOPK + lane] = m;
   }
+  stamp(3);
   char* img = reinterpret_cast<char*>(stage);
 #pragma unroll
   for (int j = 0; j < NB; ++j)
@@ -551,6 +561,7 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
   __syncthreads();   // (also: every wave's operand reads are done -- the image becomes the output stage)
   if (tid < 64) satt[tid] = kpd_sigmoid(bias2 + ((spart[0][tid] + spart[1][tid]) + (spart[2][tid] + spart[3][tid])));
   __syncthreads();
+  stamp(4);
   // x * att * 2^a as f16 hi / lo in the [hi32 | lo32] groups of the padded map's row
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -572,6 +583,10 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
   const uint4* srcs = reinterpret_cast<const uint4*>(img);
 #pragma unroll
   for (int k = 0; k < HM * 512 / 16 / 256; ++k) dst[tid + 256 * k] = srcs[tid + 256 * k];
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(5);
+  }
 }
 
 // ---------------------------------------------------------------- HeatmapHead channel attention
@@ -1018,7 +1033,7 @@ hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int
 hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk, const float* boxes, int R, int P,
                         float* roi, float* roi_stats, const void* w1s, int w1_exp, const float* b1, const float* w2,
                         const float* b2, const float* bound, int bdiv, int bstride, float* hsc, void* out,
-                        hipStream_t st) {
+                        hipStream_t st, unsigned long long* stamps) {
   if (R <= 0) return hipSuccess;
   if (!topk || !roi || !roi_stats || !w1s || !bound || bdiv < 1 || bstride < 1 || !hsc || !out)
     return hipErrorInvalidValue;
@@ -1028,7 +1043,7 @@ hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk,
   const size_t lds = std::max<size_t>((size_t)cap * 4, kRoiKhLds);
   hipLaunchKernelGGL(roi_kh_kernel, dim3(HM, R), dim3(256), lds, st, feat, Hf, Wf, topk, boxes, P, roi, roi_stats,
                      cap, static_cast<const _Float16*>(w1s), w1_exp, b1, w2, b2, bound, bdiv, bstride, hsc,
-                     static_cast<_Float16*>(out));
+                     static_cast<_Float16*>(out), stamps);
   return hipGetLastError();
 }
 hipError_t launch_hm_chattn(const float* roi_stats, int R, const float* w0, const float* b0, const float* w2,

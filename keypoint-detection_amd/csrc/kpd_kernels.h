@@ -275,7 +275,7 @@ hipError_t launch_slotmap(const float* boxes, int B, int P, int32_t* slot,
 hipError_t launch_roi_kh(const float* feat, int Hf, int Wf, const int32_t* topk, const float* boxes, int R, int P,
                         float* roi, float* roi_stats, const void* w1s, int w1_exp, const float* b1, const float* w2,
                         const float* b2, const float* bound, int bdiv, int bstride, float* hsc, void* out,
-                        hipStream_t st);
+                        hipStream_t st, unsigned long long* stamps = nullptr);
 hipError_t launch_roi_align(const float* feat, int Hf, int Wf, int Cf, const int32_t* topk,
                             const float* boxes, int R, int P, float* roi, float* roi_stats,
                             hipStream_t st, unsigned long long* stamps = nullptr);   // stamps: KPD_STAMPS [grid][8]

@@ -1706,7 +1706,8 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     if (!slot_in_topk) HIP_TRY(launch_slotmap(boxes, NB, P, w.slot, st));
     if (roi_kh)
       HIP_TRY(launch_roi_kh(w.feat, d.Hf, d.Wf, w.topk, boxes, R, P, w.roi, w.roi_stats, p->kh_sa1.ws,
-                            p->kh_sa1.w_exp, p->kh_sa1.b, p->kh_sa2_w, p->kh_sa2_b, w.imax, P, 1, w.hsc, w.kxs, st));
+                            p->kh_sa1.w_exp, p->kh_sa1.b, p->kh_sa2_w, p->kh_sa2_b, w.imax, P, 1, w.hsc, w.kxs, st,
+                            take_stamps("stamps_roikh_0", (size_t)56 * R)));
     else
       HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, w.topk, boxes, R, P, w.roi, w.roi_stats, st,
                                take_stamps("stamps_roi_0", (size_t)56 * R)));

@@ -6,6 +6,7 @@ and prints, per launch: workgroups, launch span, the workgroups alive at once
 (max / median), and the median duration of each phase of a workgroup.  The
 stamps are s_memrealtime ticks (100 MHz, 10 ns).  GPU only.
     KPD_STAMPS=1 python3 tools/stamps_probe.py
+    KPD_STAMPS=1 PROBE_PERSONS=5 python3 tools/stamps_probe.py   (dual head: roi_kh_kernel)
 """
 import os
 import sys
@@ -24,18 +25,27 @@ def main():
     from dll.models import MultiPersonKeypointModel
     from dll.models.synthetic import synthetic_boxes, synthetic_images, synthetic_state_dict
     dev = torch.device("cuda:0")
-    m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision="mixed", streams=1)
+    # PROBE_PERSONS > 1: the dual-head model in split precision (roi_kh_kernel's stamps)
+    P = int(os.environ.get("PROBE_PERSONS", "1"))
+    dual = P > 1
+    prec = "split" if dual else "mixed"
+    if dual:
+        from dll.configs import KeypointHeadConfig
+        m = MultiPersonKeypointModel(ModelConfig(keypoint_head=KeypointHeadConfig(height=56, width=56)),
+                                     TrainingConfig(), precision=prec, dual_head=True, streams=1)
+    else:
+        m = MultiPersonKeypointModel(ModelConfig(), TrainingConfig(), precision=prec, streams=1)
     m.load_state_dict(synthetic_state_dict(m.state_dict(), seed=0))
     m = m.to(dev).eval()
     B = int(os.environ.get("PROBE_BATCH", "64"))
     batch = {"image": synthetic_images(B, 3, 256, 192, seed=1234).to(dev),
-             "bboxes": synthetic_boxes(B, 1, seed=1235).to(dev)}
+             "bboxes": synthetic_boxes(B, P, seed=1235).to(dev)}
     plan = m.native_plan(dev)
     with torch.no_grad():
         for _ in range(4):
             m(batch)
     torch.cuda.synchronize()
-    names = [f"stamps_{k}_{i}" for i in range(11) for k in ("exdw", "seproj")] + ["stamps_latchain_0"] + [f"stamps_fir_{i}" for i in range(11)] + ["stamps_roi_0"]
+    names = [f"stamps_{k}_{i}" for i in range(11) for k in ("exdw", "seproj")] + ["stamps_latchain_0"] + [f"stamps_fir_{i}" for i in range(11)] + ["stamps_roi_0", "stamps_roikh_0"]
     for name in names:
         try:
             buf = plan.debug_buffer(name)
