@@ -146,6 +146,9 @@ def parse(argv=None):
     ap.add_argument("--c3-only", dest="only", action="store_const", const="C3", help="= --only C3")
     ap.add_argument("--cfg-batch", type=int, default=0, help="images per rank of the config objects (0 = theirs)")
     ap.add_argument("--cfg-cpu-sample", type=int, default=8, help="images in the config objects' CPU-baseline sample")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="test hook: initialise the process group (RCCL) and run the N-rank code paths -- "
+                         "collation, barriers, max-over-ranks timing -- even at one rank")
     ap.add_argument("--cpu-standin", action="store_true",
                     help="test mode: no GPU; gloo ranks on the CPU run a stand-in forward through the same "
                          "launcher, barrier, timing and collation code (tests/test_bench_launch.py)")
@@ -786,7 +789,7 @@ def main(argv=None):
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or (a.force_dist and "MASTER_ADDR" in os.environ)
     if a.cpu_standin:
         if dist:
             import torch.distributed as tdist

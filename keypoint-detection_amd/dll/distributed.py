@@ -14,6 +14,7 @@ the CPU tests).
 """
 from __future__ import annotations
 
+import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -53,40 +54,78 @@ class PendingCollation:
     then the caller may enqueue more work -- the next batch's forward -- which
     then overlaps the collective instead of queueing behind it."""
 
-    def __init__(self, items, group):
-        self._items = items          # key -> (work, parts, counts, send buffer kept alive)
+    def __init__(self, packs, group):
+        self._packs = packs          # [(keys, shapes, (work, out, counts, mx, widths, send buffer))]
         self._group = group
         self._done = None
 
     def wait(self) -> Dict[str, torch.Tensor]:
         if self._done is None:
             res = {}
-            for k, (work, parts, counts, _buf) in self._items.items():
-                work.wait()
-                res[k] = torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
-            self._done, self._items = res, None
+            for keys, shapes, st in self._packs:
+                st[0].wait()
+                res.update(zip(keys, _unpack(st, shapes)))
+            self._done, self._packs = res, None
         return self._done
 
 
-def _gather_start(local: torch.Tensor, total: int, group, async_op: bool):
+def _gather_start(tensors: List[torch.Tensor], total: int, group, async_op: bool):
+    """One all_gather_into_tensor of per-image tensors [n_local, ...] (same
+    dtype and device), each flattened per image and laid side by side in one
+    [n, W] send buffer: a single collective (and a single packing kernel) per
+    call instead of one gather, its list copies and a concatenation per key."""
     world = dist.get_world_size(group)
     counts = [shard_range(total, world, r) for r in range(world)]
     mx = max(b - a for a, b in counts)
-    if local.size(0) == mx:
-        buf = local.contiguous()
+    n = tensors[0].size(0)
+    flat = [t.reshape(n, math.prod(t.shape[1:])) for t in tensors]   # (explicit width: n may be 0)
+    widths = [f.size(1) for f in flat]
+    dt, dev = tensors[0].dtype, tensors[0].device
+    if len(flat) == 1 and n == mx:
+        buf = flat[0].contiguous()
     else:
-        buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        buf[: local.size(0)] = local
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    work = dist.all_gather(parts, buf, group=group, async_op=async_op)
-    return work, parts, counts, buf
+        # a short shard (uneven split) is zero padded to mx images
+        buf = (torch.empty if n == mx else torch.zeros)((mx, sum(widths)), dtype=dt, device=dev)
+        if n and sum(widths):
+            torch.cat(flat, dim=1, out=buf[:n])
+    out = torch.empty((world * mx, sum(widths)), dtype=dt, device=dev)
+    work = dist.all_gather_into_tensor(out, buf, group=group, async_op=async_op)
+    return work, out, counts, mx, widths, buf
+
+
+def _unpack(st, shapes) -> List[torch.Tensor]:
+    """[total, ...] views of the gathered [world * mx, W] buffer, one per packed
+    tensor (image-strided views: no copy when the shards are even)."""
+    _work, out, counts, mx, widths, _buf = st
+    if all(b - a == mx for a, b in counts):
+        full = out
+    else:
+        full = torch.cat([out[r * mx: r * mx + (b - a)] for r, (a, b) in enumerate(counts)], dim=0)
+    total, wsum = counts[-1][1], sum(widths)
+    res, off = [], 0
+    for w, shp in zip(widths, shapes):
+        strides, acc = [], 1
+        for d in reversed(shp):
+            strides.insert(0, acc)
+            acc *= d
+        res.append(full.as_strided((total,) + tuple(shp), (wsum,) + tuple(strides), full.storage_offset() + off))
+        off += w
+    return res
 
 
 def gather_images(local: torch.Tensor, total: int, group=None) -> torch.Tensor:
     """all_gather a per-image tensor [n_local, ...] sharded by ``shard_range``
     into [total, ...] on every rank (uneven shards padded then trimmed)."""
-    _work, parts, counts, _buf = _gather_start(local, total, group, False)
-    return torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], dim=0)
+    return _unpack(_gather_start([local], total, group, False), [tuple(local.shape[1:])])[0]
+
+
+def _packs(src: Dict[str, torch.Tensor], keys: Sequence[str], total: int, group, async_op: bool):
+    """Keys grouped by (dtype, device) in order, one packed collective per group."""
+    groups: Dict[tuple, List[str]] = {}
+    for k in keys:
+        groups.setdefault((src[k].dtype, src[k].device), []).append(k)
+    return [(ks, [tuple(src[k].shape[1:]) for k in ks], _gather_start([src[k] for k in ks], total, group, async_op))
+            for ks in groups.values()]
 
 
 def collate_outputs(out: Dict[str, torch.Tensor], total: int, group=None,
@@ -97,16 +136,19 @@ def collate_outputs(out: Dict[str, torch.Tensor], total: int, group=None,
     person).  ``max_persons``: the global padded person count when the caller
     knows it (a sharded [B,P,4] box tensor: P on every rank; the detector:
     max_persons) -- then no all_reduce and no host synchronisation happen.
+    The keys travel packed side by side in one collective per dtype.
     ``async_op``: return a PendingCollation whose ``wait()`` gives the dict
     (a serving loop collates batch k while batch k + 1 computes)."""
     p = max_persons
     if p is None:
         p = global_max_persons(out["keypoints"].size(1), out["keypoints"].device, group)
+    src = {k: pad_persons(out[k], p) for k in keys}
+    packs = _packs(src, keys, total, group, async_op)
     if async_op:
-        return PendingCollation({k: _gather_start(pad_persons(out[k], p), total, group, True) for k in keys}, group)
+        return PendingCollation(packs, group)
     res = {}
-    for k in keys:
-        res[k] = gather_images(pad_persons(out[k], p), total, group)
+    for ks, shapes, st in packs:
+        res.update(zip(ks, _unpack(st, shapes)))
     return res
 
 
