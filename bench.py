@@ -228,7 +228,8 @@ def _cuda_sync():
 
 
 def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync, finish=None):
-    """W untimed + K timed steps bracketed by barrier + synchronize; seconds.
+    """W untimed + K timed steps: barrier + synchronize, clock, the steps,
+    synchronize, clock, barrier; seconds (the max over ranks is the job time).
     finish(): completes work a step leaves in flight (the last step's result
     collation), inside the timed region, before the closing synchronize."""
     import torch.distributed as tdist
@@ -247,9 +248,14 @@ def run_steps(steps, warmup, step_fn, dist, sync=_cuda_sync, finish=None):
         if finish:
             finish()
         sync()
+        # every rank's time from the common start barrier to its own last
+        # synchronize; the job time is the max over ranks (gather_elapsed).
+        # The closing barrier follows the clock read: a RCCL barrier costs
+        # ~1.8 ms at its call, which is synchronisation, not the K steps.
+        el = time.perf_counter() - t0
         if dist:
             tdist.barrier()
-        return time.perf_counter() - t0, out
+        return el, out
 
 
 def _free_port():
