@@ -201,3 +201,57 @@ def test_collate_outputs_async_gloo():
         assert same
         assert shapes == [(7, 3, 1, 17, 2)] * 3
         assert first == [200.0 + i for i in range(7)]
+
+
+def _packed_worker(rank, world, store, q):
+    _init(rank, world, store)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "keypoint-detection_amd"))
+        from dll.distributed import collate_outputs, shard_range
+        total = 7                                        # uneven: 4 + 3 images
+        a, b = shard_range(total, world, rank)
+        n = b - a
+        idx = torch.arange(a, b, dtype=torch.float32)
+        out = {"keypoints": idx.view(n, 1, 1, 1, 1).expand(n, 2, 1, 17, 2).contiguous(),
+               "visibilities": (idx.view(n, 1, 1, 1, 1) + 0.5).expand(n, 2, 1, 17, 3).contiguous(),
+               "slot": torch.arange(a, b, dtype=torch.int64).view(n, 1).expand(n, 2).contiguous(),
+               "box_scores": (idx.view(n, 1) * 2).expand(n, 2).contiguous()}
+        keys = ("keypoints", "slot", "visibilities", "box_scores")     # mixed dtypes, interleaved
+        sync = collate_outputs(out, total, keys=keys, max_persons=3)
+        pend = collate_outputs(out, total, keys=keys, max_persons=3, async_op=True).wait()
+        res = {}
+        for k in keys:
+            assert torch.equal(sync[k], pend[k])
+            res[k] = sync[k].contiguous().numpy()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collate_outputs_packed_mixed_dtypes_gloo():
+    """The keys travel packed (one all_gather_into_tensor per dtype): every key
+    comes back with its own shape and dtype, padded to max_persons, each rank's
+    slab at its shard's offset, for uneven shards and sync / async alike."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    store = os.path.join(tempfile.mkdtemp(), "store")
+    procs = [ctx.Process(target=_packed_worker, args=(r, world, store, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _rank, r in res:
+        assert r["keypoints"].shape == (7, 3, 1, 17, 2) and r["keypoints"].dtype == np.float32
+        assert r["visibilities"].shape == (7, 3, 1, 17, 3)
+        assert r["slot"].shape == (7, 3) and r["slot"].dtype == np.int64
+        assert r["box_scores"].shape == (7, 3)
+        for i in range(7):
+            assert (r["keypoints"][i, :2] == i).all() and (r["keypoints"][i, 2] == 0).all()
+            assert (r["visibilities"][i, :2] == i + 0.5).all() and (r["visibilities"][i, 2] == 0).all()
+            assert (r["slot"][i, :2] == i).all() and r["slot"][i, 2] == 0
+            assert (r["box_scores"][i, :2] == 2 * i).all() and r["box_scores"][i, 2] == 0
