@@ -552,10 +552,7 @@ __global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float pv = wo2 * fminf(fmaxf(fmaf(am[i][e], us, bias1), 0.f), 6.f);
-      pv += __shfl_xor(pv, 1);
-      pv += __shfl_xor(pv, 2);
-      pv += __shfl_xor(pv, 4);
-      pv += __shfl_xor(pv, 8);
+      pv = row16_sum(pv);   // the 16 output channels of the wave (DPP butterfly)
       if (r16 == 0) spart[wave][i * 16 + g * 4 + e] = pv;
     }
   __syncthreads();   // (also: every wave's operand reads are done -- the image becomes the output stage)

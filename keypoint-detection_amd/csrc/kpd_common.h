@@ -58,6 +58,20 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Sum over each 16-lane row of the wave, every lane of a row receiving it: the
+// xor-1 / xor-2 / xor-4 / xor-8 butterfly on DPP lane moves (quad_perm, then
+// row_half_mirror and row_mirror, which pair a lane with one of the other
+// quad / half-row, whose lanes all hold the same partial by then), so the
+// additions -- and the result, bit for bit -- are the __shfl_xor butterfly's,
+// without its four LDS-crossbar (ds_bpermute) round trips.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
