@@ -402,6 +402,29 @@ def test_person_detector_glue_vs_oracle(precision):
     np.testing.assert_allclose(out["kh_keypoints"][sel].cpu().numpy(), ref["kh_keypoints"].numpy(), atol=tol)
 
 
+def test_person_detector_unfused_chain_vs_oracle():
+    """Level-0 rows too wide for the fused kernel's LDS (over 262 columns) take
+    the unfused detector front end (adaptive_pool56_kernel -> 1x1 heads ->
+    person_decode_kernel, the chain the fused person_detect_kernel replaces at
+    the BASELINE sizes; both pool column sums, then rows): 256 x 576 images
+    (level 0: 288 columns), checked against the oracle's glue on the GPU's
+    own FPN level 0."""
+    from dll.models.synthetic import synthetic_images
+    m, sd = _dual_model("split")
+    m.full_level0 = True
+    B, H, W = 4, 256, 576
+    img = synthetic_images(B, 3, H, W, seed=53, device=DEV)
+    with torch.no_grad():
+        out = m(img)
+    feat = m.native_plan(DEV).debug_buffer("feat0").view(B, H // 2, W // 2, 128).permute(0, 3, 1, 2).cpu()
+    got = torch.stack([out["boxes"][i].cpu() for i in range(B)])
+    got_s = out["box_scores"].cpu()
+    assert got.shape == (B, 5, 4)
+    assert (got_s > 0).any(), "no person detected"
+    ref_boxes, ref_scores = O.person_detect(feat, sd, H, W, 0.3, 0.3, 5)
+    _check_detections(got, got_s, ref_boxes, ref_scores, "unfused glue on the GPU's level 0")
+
+
 def _predict_module():
     import sys
     from conftest import PKG
