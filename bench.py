@@ -365,10 +365,13 @@ def main_standin(a, world, rank, dist):
             "unit": "images/s", "n_gpus": world, "world": world, "backend": "gloo" if dist else None,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4),
             "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+            "rccl_ranks": rank_census(dist, torch.device("cpu")),
             "collated": {k: list(v.shape) for k, v in coll.items()}}
     if gather:   # every rank's slab landed at its shard's offset
         from dll.distributed import shard_range
-        line["collated_ok"] = bool(all(
+        line["collated_ok"] = collation_check(model(batch), coll, ("keypoints", "visibilities"), P, world, rank,
+                                              dist, torch.device("cpu"))
+        line["collated_index_ok"] = bool(all(
             torch.equal(coll["visibilities"][s:e, :, 0, :, 2], torch.ones(e - s, P, 17))
             for s, e in (shard_range(B * world, world, r) for r in range(world))))
     cfgs = {}
@@ -380,6 +383,19 @@ def main_standin(a, world, rank, dist):
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def rank_census(dist, dev):
+    """Ranks in the process group, counted by an all_reduce(SUM) of ones over
+    the data-path backend (RCCL on the GPU ranks, gloo for the stand-in): a
+    self-check that every rank took part in the collectives; None without a
+    process group."""
+    if not dist:
+        return None
+    import torch.distributed as tdist
+    t = torch.ones(1, device=dev, dtype=torch.int32)
+    tdist.all_reduce(t)
+    return int(t.item())
 
 
 def gather_elapsed(el, world, dist, dev):
@@ -610,7 +626,8 @@ def run_pipeline(name, a, dev, pmc, world=1, rank=0, dist=False, cpu=True, stand
     el = max(per_rank)
     res.update({"value": round(gN * a.steps / el, 2), "unit": "images/s", "ms_per_step": round(el / a.steps * 1e3, 4),
                 "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
-                "steps": a.steps, "warmup": a.warmup, "streams_per_gpu": 1, "scaling": "weak"})
+                "steps": a.steps, "warmup": a.warmup, "streams_per_gpu": 1, "scaling": "weak",
+                "rccl_ranks": rank_census(dist, dev)})
     if gather:
         res["collated"] = {k: list(v.shape) for k, v in coll.items()}
         res["collated_ok"] = collation_check(out if "boxes" not in keys else dict(out, boxes=out["boxes_t"]),
@@ -893,6 +910,7 @@ def main(argv=None):
         "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "rank_ms_per_step": [round(t / a.steps * 1e3, 4) for t in per_rank],
+        "rccl_ranks": rank_census(dist, dev),
         "dtype": dtypes[a.precision][0], "dtype_detail": dtypes[a.precision][1],
         "data": "synthetic (seeded U[0,1) images ImageNet-normalised, seeded boxes, seed-0 random weights)",
         "config": {"workload": f"C2: batch {B}/GPU, {a.height}x{a.width}x3, {P} box/img, heatmap head + "
@@ -911,6 +929,9 @@ def main(argv=None):
                        "boundary (so the stages sum to more than a step), and ms_per_step is a wall-clock mean",
         "cpu_baseline": None,
     }
+    if gather:   # every rank's keypoint / visibility slab at its shard's offset in every rank's collated copy
+        line["collated"] = {k: list(v.shape) for k, v in coll.items()}
+        line["collated_ok"] = collation_check(out, coll, ("keypoints", "visibilities"), P, world, rank, dist, dev)
     if world == 1 and a.alt_streams and a.alt_streams != a.streams and B // 16 >= 2:
         # the same model, batch and precision as concurrent sub-batches (kpd_plan_set_streams): the
         # sub-batches' kernels overlap, so this is a throughput figure only (no per-kernel timing)

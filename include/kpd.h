@@ -251,6 +251,21 @@ int kpd_keypoint_head(kpd_plan* plan, const float* x, int R, int H, int W, float
 int kpd_backbone(kpd_plan* plan, const float* image, int B, int C, int H, int W, float* out0, float* out1,
                  float* out2, float* out3, void* stream);
 
+/* MobileNetV3Wrapper.body(x) (backbone.py:250-254: create_feature_extractor
+ * over mobilenet_v3_small, return_nodes features.0 / .3 / .8 / .12):
+ * image [B][C][H][W] -> feat0 [B][16][h0][w0], feat1 [B][24][h3][w3],
+ * feat2 [B][48][h8][w8], feat3 [B][576][h11][w11] (strides 2, 8, 16, 32). */
+int kpd_backbone_body(kpd_plan* plan, const float* image, int B, int C, int H, int W, float* feat0, float* feat1,
+                      float* feat2, float* feat3, void* stream);
+
+/* LightweightFPN.forward (backbone.py:29-39) on caller taps feat_i
+ * [B][c_i][h_i][w_i], c = 16, 24, 48, 576; sizes = {h0, w0, h1, w1, h2, w2,
+ * h3, w3} (host array).  Lateral i+1 is nearest-resized to (h_i, w_i) and added to lateral
+ * i (F.interpolate 'nearest' indexing); out_i [B][128][h_i][w_i] = fpn_convs[i]
+ * (3x3 + BN + ReLU) of lateral i, exact fp32 products. */
+int kpd_backbone_fpn(kpd_plan* plan, const float* feat0, const float* feat1, const float* feat2, const float* feat3,
+                     int B, const int* sizes, float* out0, float* out1, float* out2, float* out3, void* stream);
+
 /* ChannelAttention.forward (keypoint_model.py:33-44) on x [B][128][H][W] ->
  * scores [B][128] (sigmoid); select_top_k_channels (:653-661): topk [B][k]
  * int32 (descending score, ties to the lower index) and selected

@@ -203,18 +203,31 @@ __global__ __launch_bounds__(256) void k6_amax_kernel(const float* __restrict__ 
     atomicMax(reinterpret_cast<unsigned*>(hsc + (size_t)blockIdx.y * 4), __float_as_uint(m));
 }
 
-// hsc[n][1] = hsc[n][0] * 2^-w_exp: the bound whose split_exp_of is a + w_exp
-// (a = split_exp_of(max |x_n|), the input scale of k6_to_hm_kernel), so that
-// hmconv_kernel (in_idx 1, w_exp 0) unscales by 2^-(a + w_exp) with the
-// weights' exponent computed on the device (no host round trip)
+// Per image n: the input scale exponent a (hsc[n][2], an exact small integer
+// as float: k6_to_hm_kernel scales by 2^a) and hsc[n][1], the bound whose
+// split_exp_of is a + w_exp, so that hmconv_kernel (in_idx 1, w_exp 0)
+// unscales by 2^-(a + w_exp) with the weights' exponent computed on the
+// device (no host round trip).  a = split_exp_of(max |x_n|), lowered where
+// a + w_exp would pass split_exp_of's clamp at 100 (max|x| * max|w| below
+// ~2^-72): then hsc[n][1] = 0, whose split_exp_of is 100 = a + w_exp exactly
+// (a smaller scale only lowers the split's precision floor).
 __global__ __launch_bounds__(256) void k6_bound_kernel(float* __restrict__ hsc, int N, const float* __restrict__ wmax) {
   const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n < N) hsc[(size_t)n * 4 + 1] = ldexpf(hsc[(size_t)n * 4], -split_exp_of(*wmax));
+  if (n >= N) return;
+  const int we = split_exp_of(*wmax);
+  int a = split_exp_of(hsc[(size_t)n * 4]);
+  float bound = ldexpf(hsc[(size_t)n * 4], -we);
+  if (a + we > 100) {
+    a = 100 - we;
+    bound = 0.f;
+  }
+  hsc[(size_t)n * 4 + 1] = bound;
+  hsc[(size_t)n * 4 + 2] = (float)a;
 }
 
 // x [N][C][56][56] fp32 -> the hmconv split layout [N * 3249][C / 32][hi32 | lo32]
 // f16 at interior positions (borders zeroed by the caller), image n scaled by
-// 2^split_exp_of(hsc[n * 4]) -- the scale hmconv_kernel's split mode unscales by
+// 2^hsc[n * 4 + 2] (k6_bound_kernel) -- the scale hmconv_kernel's split mode unscales by
 __global__ __launch_bounds__(256) void k6_to_hm_kernel(const float* __restrict__ x, int C,
                                                        const float* __restrict__ hsc, _Float16* __restrict__ out) {
   __shared__ float t[32][65];
@@ -227,7 +240,7 @@ __global__ __launch_bounds__(256) void k6_to_hm_kernel(const float* __restrict__
   __syncthreads();
   const int pp = tid >> 2, c8 = (tid & 3) * 8, p = p0 + pp;
   if (p >= kHmSide * kHmSide) return;
-  const float sc = ldexpf(1.f, split_exp_of(hsc[(size_t)n * 4]));
+  const float sc = ldexpf(1.f, (int)hsc[(size_t)n * 4 + 2]);
   const int y = p / kHmSide, xx = p - y * kHmSide;
   f16x8 hi, lo;
 #pragma unroll
@@ -612,12 +625,12 @@ static hipError_t k6_split_conv(const float* x, const float* w, const float* b, 
     }
     const long per_img = (long)cin * kHmSide * kHmSide;
     hipLaunchKernelGGL(k6_amax_kernel, dim3(64, (unsigned)N), dim3(256), 0, st, x, per_img, hsc);
-    hipLaunchKernelGGL(k6_to_hm_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)(cin / 32), (unsigned)N), dim3(256),
-                       0, st, x, cin, hsc, hm);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = hipMemsetAsync(mx, 0, sizeof(float), st)) != hipSuccess) break;
     hipLaunchKernelGGL(k6_max_kernel, dim3(64), dim3(256), 0, st, w, (long)cin * cout * 9, mx);
     hipLaunchKernelGGL(k6_bound_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, hsc, N, mx);
+    hipLaunchKernelGGL(k6_to_hm_kernel, dim3((kHmSide * kHmSide + 63) / 64, (unsigned)(cin / 32), (unsigned)N), dim3(256),
+                       0, st, x, cin, hsc, hm);
     const long nw = (long)cout_p * 9 * cin;
     hipLaunchKernelGGL(k6_pack_w_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, w, flip ? cin : cout,
                        flip ? cout : cin, flip, mx, cout_p, ws);

@@ -2132,6 +2132,9 @@ static hipError_t launch_hmconv_kh(const HmConvArgs& a0, hipStream_t st) {
                 : (a0.cin == 64 && a0.cout == 64 && a0.ntap == 10) ? 2
                 : (a0.cin == 32 && a0.cout == 64 && a0.ntap == 9) ? 3 : 0;
   if (!sel) return hipErrorInvalidValue;
+  // the staged BN = 128 epilogue adds the downsample (tenth-tap) accumulator
+  // to columns 0..63 only: a wider identity branch is not expressible there
+  if (sel == 1 && a0.ns > 64) return hipErrorInvalidValue;
   HmConvArgs a = a0;
   const long wt_bytes = (long)a.cout * a.ntap * a.cin * 4, roi_bytes = (long)HPP * a.cin * 4;
   if (wt_bytes > kMaxDesc) return hipErrorInvalidValue;

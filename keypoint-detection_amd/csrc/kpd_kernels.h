@@ -350,6 +350,9 @@ hipError_t launch_roi_align_nchw(const float* feat, int C, int H, int W, const f
 hipError_t launch_nchw_rows_to_nhwc(const float* in, int N, int C, int H, int W, float* out, float* stats,
                                     hipStream_t st, float* amax = nullptr, int amax_stride = 0);
 hipError_t launch_nhwc_to_nchw(const float* in, int N, int HW, int C, float* out, hipStream_t st);
+// padded-channel NHWC <-> NCHW (any C <= Cp; the padding channels written as zero)
+hipError_t launch_nhwc_pad_to_nchw(const float* in, int N, int HW, int C, int Cp, float* out, hipStream_t st);
+hipError_t launch_nchw_to_nhwc_pad(const float* in, int N, int HW, int C, int Cp, float* out, hipStream_t st);
 hipError_t launch_nchw_channel_stats(const float* x, int N, int C, int HW, float* stats, hipStream_t st);
 hipError_t launch_gather_planes(const float* x, int N, int C, int HW, const int32_t* idx, int K, float* out,
                                 hipStream_t st);

@@ -234,6 +234,10 @@ struct kpd_plan {
   // passes a stage mark, so its latency-bound body overlaps k's heavy stages
   hipEvent_t pipe_ev[kMaxSub] = {};
   bool keep_laterals = false;   // kpd_backbone: every lateral level is an output (no fused chain)
+  // kpd_backbone_body: the forward stops after the MobileNet body; its four
+  // taps (NHWC, channels padded to 16) are left in the workspace here
+  bool body_only = false;
+  const float* body_taps[4] = {};
   // hipGraph replay of whole forwards (KPD_GRAPH=1): one executable graph per
   // call signature (shapes, flags, every buffer address, stream), valid while
   // the workspace carve and the weights are the ones it was captured on
@@ -1554,6 +1558,10 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     return rc;
   taps[3] = w.last;
   body_stage.reset();
+  if (p->body_only) {   // kpd_backbone_body
+    for (int i = 0; i < 4; ++i) p->body_taps[i] = taps[i];
+    return KPD_OK;
+  }
   if (int rc = mark(1)) return rc;
 
   // ---------------- FPN laterals (top-down) + level-0 3x3 ----------------
@@ -1728,9 +1736,11 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
     Stage sg(p, "keypoint_head", st);
     if (!roi_kh) HIP_TRY(launch_roi_align(w.feat, d.Hf, d.Wf, 128, nullptr, boxes, R, P, w.kx, nullptr, st));
     const long khrows = (long)R * kHmRoiPos - kHmPitch;
+    // sized for 256-row tiles, the smallest launch_hmconv_kh picks (KPD_KH_BM256 /
+    // KPD_KH_TPS1 take them for every conv; by default convs 2 / 3 use 384 / 512)
     unsigned long long* khst[3] = {take_stamps("stamps_kh1", (size_t)((khrows + 255) / 256)),
-                                   take_stamps("stamps_kh2", (size_t)((khrows + 383) / 384)),
-                                   take_stamps("stamps_kh3", (size_t)((khrows + 511) / 512))};
+                                   take_stamps("stamps_kh2", (size_t)((khrows + 255) / 256)),
+                                   take_stamps("stamps_kh3", (size_t)((khrows + 255) / 256))};
     if (int rc = run_keypoint_head(p, w, R, P, kh_kpts, kh_vis, st, w.imax, P, 1, roi_kh, khst)) return rc;
   }
   return KPD_OK;
@@ -2100,6 +2110,102 @@ int kpd_backbone(kpd_plan* p, const float* image, int B, int C, int H, int W, fl
     }
   }
   return KPD_OK;
+}
+
+int kpd_backbone_body(kpd_plan* p, const float* image, int B, int C, int H, int W, float* feat0, float* feat1,
+                      float* feat2, float* feat3, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_body) return fail(KPD_ESTATE, "plan lacks backbone.body weights");
+  if (!image || B <= 0 || H < 32 || W < 32) return fail(KPD_EINVAL, "bad image shape");
+  if (C != p->in_ch) return fail(KPD_EINVAL, "image channels do not match backbone in_channels");
+  float* outs[4] = {feat0, feat1, feat2, feat3};
+  for (float* o : outs)
+    if (!o) return fail(KPD_EINVAL, "null output pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  int h[12], wd[12];
+  h[0] = (H - 1) / 2 + 1; wd[0] = (W - 1) / 2 + 1;
+  for (int i = 0; i < 11; ++i) {
+    const int k = kBneck[i].k, s = kBneck[i].s, pd = (k - 1) / 2;
+    h[i + 1] = (h[i] + 2 * pd - k) / s + 1;
+    wd[i + 1] = (wd[i] + 2 * pd - k) / s + 1;
+  }
+  const int lv[4] = {0, 3, 8, 11};
+  const int cap = max_pass_images(H, W), npass = (B + cap - 1) / cap;
+  for (int q = 0; q < npass; ++q) {
+    const int b0 = (int)((long)B * q / npass), b1 = (int)((long)B * (q + 1) / npass), nb = b1 - b0;
+    p->body_only = true;
+    const int rc1 = forward_one(p, 0, false, image + (size_t)b0 * C * H * W, nb, C, H, W, nullptr, 0, 0, 0, nullptr,
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, st);
+    p->body_only = false;
+    if (rc1) return rc1;
+    for (int i = 0; i < 4; ++i) {
+      const int c = kFpnIn[i], hw = h[lv[i]] * wd[lv[i]];
+      HIP_TRY(launch_nhwc_pad_to_nchw(p->body_taps[i], nb, hw, c, pad16(c), outs[i] + (size_t)b0 * c * hw, st));
+    }
+  }
+  return KPD_OK;
+}
+
+int kpd_backbone_fpn(kpd_plan* p, const float* feat0, const float* feat1, const float* feat2, const float* feat3, int B,
+                     const int* sizes, float* out0, float* out1, float* out2, float* out3, void* stream) {
+  if (!p || !p->finalized) return fail(KPD_ESTATE, "plan not finalized");
+  if (!p->has_fpn) return fail(KPD_ESTATE, "plan lacks backbone.fpn weights");
+  for (int i = 0; i < 3; ++i)
+    if (!p->fpn_lv[i].w) return fail(KPD_ESTATE, "plan lacks backbone.fpn.fpn_convs.1-3 weights");
+  if (B < 0 || !sizes) return fail(KPD_EINVAL, "bad FPN arguments");
+  if (B == 0) return KPD_OK;
+  const float* feats[4] = {feat0, feat1, feat2, feat3};
+  float* outs[4] = {out0, out1, out2, out3};
+  int hh[4], ww[4];
+  size_t in_f = 0, lat_f = 0, out_f = 0;
+  for (int i = 0; i < 4; ++i) {
+    hh[i] = sizes[2 * i]; ww[i] = sizes[2 * i + 1];
+    if (!feats[i] || !outs[i]) return fail(KPD_EINVAL, "null FPN tensor");
+    if (hh[i] <= 0 || ww[i] <= 0) return fail(KPD_EINVAL, "bad FPN level size");
+    if (p->lat[i].cin != kFpnIn[i]) return fail(KPD_EINVAL, "lateral conv channels do not match the taps");
+    const size_t hw = (size_t)B * hh[i] * ww[i];
+    if (hw * 576 >= (1UL << 31)) return fail(KPD_EINVAL, "FPN tensors must stay below 2^31 elements");
+    in_f += hw * p->lat[i].cin_p;
+    lat_f += hw * 128;
+    out_f = std::max(out_f, hw * 128);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipSetDevice(p->device));
+  float* scratch = nullptr;
+  const size_t total = in_f + lat_f + out_f + kSplitKFloats;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), total * sizeof(float), st));
+  float *tin[4], *lat[4];
+  float* cur = scratch;
+  for (int i = 0; i < 4; ++i) { tin[i] = cur; cur += (size_t)B * hh[i] * ww[i] * p->lat[i].cin_p; }
+  for (int i = 0; i < 4; ++i) { lat[i] = cur; cur += (size_t)B * hh[i] * ww[i] * 128; }
+  float* lvl = cur;
+  cur += out_f;
+  g_splitk = cur;
+  // LightweightFPN.forward (backbone.py:29-39): laterals top-down, each
+  // nearest-upsampled to the next finer size and added, then fpn_convs[i]
+  int rc = KPD_OK;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 4 && e == hipSuccess; ++i)
+    e = launch_nchw_to_nhwc_pad(feats[i], B, hh[i] * ww[i], kFpnIn[i], p->lat[i].cin_p, tin[i], st);
+  for (int i = 3; i >= 0 && e == hipSuccess && rc == KPD_OK; --i) {
+    const float* res = i < 3 ? lat[i + 1] : nullptr;
+    const int rh = i < 3 ? hh[i + 1] : 0, rw = i < 3 ? ww[i + 1] : 0;
+    if (i == 0 && p->lat[i].cin_p <= 32)   // the 16-channel stem tap (as forward_one)
+      e = launch_lateral_stream(tin[i], p->lat[i].cin_p, (const float*)p->lat[i].w, p->lat[i].b, res, B, hh[i], ww[i],
+                                rh, rw, lat[i], st);
+    else
+      rc = conv(p->lat[i], tin[i], B, hh[i], ww[i], p->lat[i].cin_p, lat[i], ACT_NONE, res, rh, rw, nullptr, nullptr, 0,
+                0, st);
+  }
+  for (int i = 0; i < 4 && e == hipSuccess && rc == KPD_OK; ++i) {
+    const DevConv& L = i == 0 ? p->fpn0 : p->fpn_lv[i - 1];
+    rc = conv(L, lat[i], B, hh[i], ww[i], 128, lvl, ACT_RELU, nullptr, 0, 0, nullptr, nullptr, 0, 0, st);
+    if (rc == KPD_OK) e = launch_nhwc_to_nchw(lvl, B, hh[i] * ww[i], 128, outs[i], st);
+  }
+  (void)hipFreeAsync(scratch, st);
+  HIP_TRY(e);
+  return rc;
 }
 
 int kpd_channel_attention(kpd_plan* p, const float* x, int B, int C, int H, int W, float* scores, int32_t* topk,

@@ -236,6 +236,43 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float* __restri
   }
 }
 
+// [N][HW][Cp] (channels padded to Cp) -> [N][C][HW]: a 32-pixel x 32-channel
+// tile per workgroup (grid: pixel tiles, channel tiles, images); the body taps
+// of MobileNetV3Wrapper.body (up to 576 channels)
+__global__ __launch_bounds__(256) void nhwc_pad_to_nchw_kernel(const float* __restrict__ in, int HW, int C, int Cp,
+                                                               float* __restrict__ out) {
+  __shared__ float t[32][33];
+  const int p0 = blockIdx.x * 32, c0 = blockIdx.y * 32, n = blockIdx.z, tid = threadIdx.x;
+  const int np = min(32, HW - p0), nc = min(32, C - c0);
+  for (int e = tid; e < 32 * 32; e += 256) {
+    const int p = e >> 5, c = e & 31;
+    if (p < np && c < nc) t[p][c] = in[((size_t)n * HW + p0 + p) * Cp + c0 + c];
+  }
+  __syncthreads();
+  for (int e = tid; e < 32 * 32; e += 256) {
+    const int c = e >> 5, p = e & 31;
+    if (p < np && c < nc) out[((size_t)n * C + c0 + c) * HW + p0 + p] = t[p][c];
+  }
+}
+
+// [N][C][HW] -> [N][HW][Cp], zero in the padding channels C..Cp-1 (the body
+// layout the FPN convs read: LightweightFPN.forward on caller taps)
+__global__ __launch_bounds__(256) void nchw_to_nhwc_pad_kernel(const float* __restrict__ in, int HW, int C, int Cp,
+                                                               float* __restrict__ out) {
+  __shared__ float t[32][33];
+  const int p0 = blockIdx.x * 32, c0 = blockIdx.y * 32, n = blockIdx.z, tid = threadIdx.x;
+  const int np = min(32, HW - p0), nc = min(32, Cp - c0);
+  for (int e = tid; e < 32 * 32; e += 256) {
+    const int c = e >> 5, p = e & 31;
+    if (p < np && c < nc) t[p][c] = c0 + c < C ? in[((size_t)n * C + c0 + c) * HW + p0 + p] : 0.f;
+  }
+  __syncthreads();
+  for (int e = tid; e < 32 * 32; e += 256) {
+    const int p = e >> 5, c = e & 31;
+    if (p < np && c < nc) out[((size_t)n * HW + p0 + p) * Cp + c0 + c] = t[p][c];
+  }
+}
+
 // per (image, channel) plane: sum and max over HW -> stats [N][1][2][C]
 // (the layout topk_kernel reads, one "tile" per image)
 __global__ __launch_bounds__(256) void nchw_channel_stats_kernel(const float* __restrict__ x, int C, int HW,
@@ -344,6 +381,22 @@ hipError_t launch_nhwc_to_nchw(const float* in, int N, int HW, int C, float* out
   if (N <= 0 || HW <= 0) return hipSuccess;
   if (C > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3((HW + 31) / 32, N), dim3(256), 0, st, in, HW, C, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_nhwc_pad_to_nchw(const float* in, int N, int HW, int C, int Cp, float* out, hipStream_t st) {
+  if (N <= 0 || HW <= 0 || C <= 0) return hipSuccess;
+  if (Cp < C || N > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(nhwc_pad_to_nchw_kernel, dim3((HW + 31) / 32, (C + 31) / 32, N), dim3(256), 0, st, in, HW, C, Cp,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_nchw_to_nhwc_pad(const float* in, int N, int HW, int C, int Cp, float* out, hipStream_t st) {
+  if (N <= 0 || HW <= 0 || Cp <= 0) return hipSuccess;
+  if (Cp < C || N > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel, dim3((HW + 31) / 32, (Cp + 31) / 32, N), dim3(256), 0, st, in, HW, C, Cp,
+                     out);
   return hipGetLastError();
 }
 

@@ -32,7 +32,7 @@ EXPORTS = ("kpd_last_error", "kpd_version", "kpd_plan_create", "kpd_plan_set_ten
            "kpd_plan_set_streams", "kpd_preprocess", "kpd_target_heatmaps", "kpd_keypoint_metrics",
            "kpd_heatmap_head", "kpd_keypoint_head", "kpd_backbone", "kpd_channel_attention", "kpd_decode_heatmaps",
            "kpd_roi_align", "kpd_conv1x1", "kpd_adaptive_heatmap_loss", "kpd_conv3x3_forward",
-           "kpd_conv3x3_backward", "kpd_plan_set_graphs")
+           "kpd_conv3x3_backward", "kpd_plan_set_graphs", "kpd_backbone_body", "kpd_backbone_fpn")
 FLAG_DETECT = 1
 FLAG_DUAL_HEAD = 2
 FLAG_FULL_LEVEL0 = 4   # store all of FPN level 0 (debug copy "feat0"); default: only the ROI-align footprints
@@ -93,6 +93,10 @@ def load() -> ctypes.CDLL:
     lib.kpd_keypoint_head.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]
     lib.kpd_backbone.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p]
+    lib.kpd_backbone_body.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]
+    lib.kpd_backbone_fpn.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                     ctypes.POINTER(c_int), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kpd_channel_attention.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                           c_void_p, c_void_p]
     lib.kpd_decode_heatmaps.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
@@ -229,16 +233,37 @@ class Plan:
     def backbone(self, image: torch.Tensor):
         image = _dev_f32(image, "image")
         B, C, H, W = image.shape
-        h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-        sizes = [(h, w)]
-        for k, s_ in ((3, 2), (3, 2), (3, 1), (5, 2), (5, 1), (5, 1), (5, 1), (5, 1), (5, 2), (5, 1), (5, 1)):
-            pd = (k - 1) // 2
-            h, w = (h + 2 * pd - k) // s_ + 1, (w + 2 * pd - k) // s_ + 1
-            sizes.append((h, w))
+        sizes = _level_sizes(H, W)
         outs = [torch.empty(B, 128, *sizes[i], device=image.device) for i in (0, 3, 8, 11)]
         with torch.cuda.device(self.device):
             check(self.lib.kpd_backbone(self.h, _ptr(image), B, C, H, W, *[_ptr(o) for o in outs],
                                         _stream(self.device)), "kpd_backbone")
+        return outs
+
+    def body_taps(self, image: torch.Tensor):
+        """MobileNetV3Wrapper.body(x): the four taps feat0..feat3 [B,c,h,w]
+        (c = 16, 24, 48, 576 at strides 2, 8, 16, 32) -- kpd_backbone_body."""
+        image = _dev_f32(image, "image")
+        B, C, H, W = image.shape
+        sizes = _level_sizes(H, W)
+        outs = [torch.empty(B, c, *sizes[i], device=image.device) for c, i in zip((16, 24, 48, 576), (0, 3, 8, 11))]
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_backbone_body(self.h, _ptr(image), B, C, H, W, *[_ptr(o) for o in outs],
+                                             _stream(self.device)), "kpd_backbone_body")
+        return outs
+
+    def fpn(self, feats):
+        """LightweightFPN.forward on four caller taps [B,c_i,h_i,w_i] -> four
+        [B,128,h_i,w_i] levels (kpd_backbone_fpn)."""
+        feats = [_dev_f32(f, f"features[{i}]") for i, f in enumerate(feats)]
+        B = feats[0].shape[0]
+        if any(f.dim() != 4 or f.shape[0] != B for f in feats):
+            raise ValueError("FPN features must be [B, C, H, W] with one batch size")
+        sizes = (ctypes.c_int * 8)(*[v for f in feats for v in f.shape[2:]])
+        outs = [torch.empty(B, 128, *f.shape[2:], device=f.device) for f in feats]
+        with torch.cuda.device(self.device):
+            check(self.lib.kpd_backbone_fpn(self.h, *[_ptr(f) for f in feats], B, sizes, *[_ptr(o) for o in outs],
+                                            _stream(self.device)), "kpd_backbone_fpn")
         return outs
 
     def channel_attention(self, x: torch.Tensor, k: int = 64, select: bool = False):
@@ -261,6 +286,17 @@ class Plan:
         check(self.lib.kpd_debug_copy(self.h, name.encode(), _ptr(out), n.value, None, _stream(self.device)),
               "kpd_debug_copy")
         return out
+
+
+def _level_sizes(H: int, W: int):
+    """(h, w) of the stem output and of features.1..11 (torchvision conv arithmetic)."""
+    h, w = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    sizes = [(h, w)]
+    for k, s_ in ((3, 2), (3, 2), (3, 1), (5, 2), (5, 1), (5, 1), (5, 1), (5, 1), (5, 2), (5, 1), (5, 1)):
+        pd = (k - 1) // 2
+        h, w = (h + 2 * pd - k) // s_ + 1, (w + 2 * pd - k) // s_ + 1
+        sizes.append((h, w))
+    return sizes
 
 
 def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:

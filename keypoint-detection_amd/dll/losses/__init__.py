@@ -1,3 +1,5 @@
-from .keypoint_loss import AdaptiveHeatmapLoss
+from .keypoint_loss import (AdaptiveHeatmapLoss, DynamicLossBalancer, ImprovedKeypointLoss, KeypointLoss, LossMetrics,
+                            SpatialCoordinateLoss)
 
-__all__ = ["AdaptiveHeatmapLoss"]
+__all__ = ["AdaptiveHeatmapLoss", "DynamicLossBalancer", "ImprovedKeypointLoss", "KeypointLoss", "LossMetrics",
+           "SpatialCoordinateLoss"]

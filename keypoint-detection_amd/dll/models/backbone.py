@@ -5,13 +5,15 @@ from torchvision's mobilenet_v3_small via ``create_feature_extractor``;
 ``backbone.fpn.{lateral_convs,fpn_convs}``) so that reference checkpoints load
 unchanged.  ``MobileNetV3Wrapper.forward`` runs the native HIP plan
 (kpd_backbone: csrc/ folds BN and repacks to NHWC at load time) and returns
-the four FPN levels as the reference does; the body and the FPN are one fused
-path there, so their separate forwards name that entry point.
+the four FPN levels as the reference does.  ``body(x)`` (the feature
+extractor's four taps, kpd_backbone_body) and ``fpn(taps)`` (kpd_backbone_fpn)
+are native on their own too, for callers of the reference's sub-modules.
 
 Reference: dll/models/backbone.py:7-39 (LightweightFPN), :247-264
 (MobileNetV3Wrapper); torchvision mobilenet_v3_small topology restated in
 oracle/kpd_oracle.py:MBV3_SMALL_BNECK.
 """
+from collections import OrderedDict
 from typing import List
 
 import torch.nn as nn
@@ -75,9 +77,17 @@ class InvertedResidual(nn.Module):
 class MobileNetV3SmallBody(nn.Module):
     """features.0..12 of mobilenet_v3_small (the part create_feature_extractor keeps)."""
 
+    RETURN_NODES = (("features.0", "feat0"), ("features.3", "feat1"), ("features.8", "feat2"),
+                    ("features.12", "feat3"))
+
     def forward(self, x):
-        raise NotImplementedError("the MobileNetV3-Small body runs fused with the FPN in the native plan: "
-                                  "call MobileNetV3Wrapper.forward (model.backbone(x))")
+        """The feature extractor's call (backbone.py:253-254, 259): x [B,C,H,W] ->
+        OrderedDict feat0 [B,16,H/2,W/2], feat1 [B,24,H/8,W/8], feat2
+        [B,48,H/16,W/16], feat3 [B,576,H/32,W/32] (kpd_backbone_body; eval only)."""
+        if self.training:
+            raise NotImplementedError("the backbone runs the eval path only; call .eval()")
+        taps = self._plans.get(self, x.device, "fp32").body_taps(x)
+        return OrderedDict((name, t) for (_, name), t in zip(self.RETURN_NODES, taps))
 
     def __init__(self, in_channels: int = 3):
         super().__init__()
@@ -86,12 +96,18 @@ class MobileNetV3SmallBody(nn.Module):
             mods.append(InvertedResidual(cin, k, exp, cout, se, s))
         mods.append(ConvBN(96, 576, 1))
         self.features = nn.Sequential(*mods)
+        self._plans = _native.PlanCache("backbone.body.", in_channels)
 
 
 class LightweightFPN(nn.Module):
     def forward(self, features):
-        raise NotImplementedError("the FPN runs fused with the body in the native plan: call "
-                                  "MobileNetV3Wrapper.forward (model.backbone(x))")
+        """features: the four taps [B,c_i,h_i,w_i] -> four [B,128,h_i,w_i] levels
+        (backbone.py:29-39; kpd_backbone_fpn, eval only)."""
+        if len(features) != len(self.lateral_convs):
+            raise ValueError(f"Expected {len(self.lateral_convs)} features, got {len(features)}")
+        if self.training:
+            raise NotImplementedError("the FPN runs the eval path only; call .eval()")
+        return self._plans.get(self, features[0].device, "fp32").fpn(list(features))
 
     def __init__(self, in_channels_list, out_channels):
         super().__init__()
@@ -103,6 +119,7 @@ class LightweightFPN(nn.Module):
             nn.Sequential(nn.Conv2d(out_channels, out_channels, 3, 1, 1, bias=False),
                           nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True))
             for _ in in_channels_list])
+        self._plans = _native.PlanCache("backbone.fpn.")
 
 
 class MobileNetV3Wrapper(nn.Module):

@@ -27,6 +27,7 @@ import torch.nn as nn
 from .. import _native
 from ..configs.model_config import ModelConfig
 from ..configs.training_config import TrainingConfig
+from ..losses import KeypointLoss
 from .backbone import MobileNetV3Wrapper
 from .heatmap_head import HeatmapHead
 from .keypoint_head import KEYPOINT_HEAD
@@ -135,6 +136,9 @@ class MultiPersonKeypointModel(nn.Module):
         self.person_detector = PERSON_HEAD(config.person_head)
         self.heatmap_head = HeatmapHead(config.heatmap_head)
         self.channel_attention = ChannelAttention(config.backbone.out_channels, reduction_ratio=16)
+        # no parameters: the state dict is unchanged (reference :65-69)
+        self.loss_fn = KeypointLoss(num_keypoints=config.num_keypoints, config=training_config,
+                                    device=torch.device("cuda"))
         self.dual_head = dual_head
         if dual_head:
             self.keypoint_head = KEYPOINT_HEAD(config.keypoint_head)
@@ -205,16 +209,65 @@ class MultiPersonKeypointModel(nn.Module):
             m.precision = value
 
     def forward(self, batch) -> Dict[str, torch.Tensor]:
+        """The eval forward (reference :73-210).  A dict batch that also
+        carries 'keypoints' and 'visibilities' (the trainer's validation
+        loop) gets the loss and its components added (:208-209, 509-584):
+        the heatmap term on the device, the balancer's state advancing per
+        call as in the reference."""
+        out = self._forward(batch)
+        if isinstance(batch, dict) and "keypoints" in batch and "visibilities" in batch:
+            out = self._compute_loss_and_metrics(out, batch)
+        return out
+
+    def _compute_loss_and_metrics(self, outputs, batch):
+        """Reference :509-584: the person axis is max-reduced for the heatmaps
+        and visibilities (prediction and target), the keypoints keep it; the
+        target heatmaps are batch['heatmaps'] or zeros of
+        heatmap_head.heatmap_size."""
+        K = self.num_keypoints
+        hs = tuple(self.config.heatmap_head.heatmap_size)
+        ph = outputs["heatmap"]
+        if ph.dim() == 5:
+            ph = ph.max(dim=1)[0]
+        elif ph.dim() != 4:
+            ph = ph.reshape(ph.size(0) if ph.dim() == 3 else batch["image"].size(0), K, *hs)
+        if "heatmaps" in batch:
+            gh = batch["heatmaps"]
+            if gh.dim() == 5:
+                gh = gh.max(dim=1)[0]
+        else:
+            gh = torch.zeros(batch["image"].size(0), K, *hs, device=batch["image"].device, dtype=torch.float32)
+        if tuple(gh.shape) != tuple(ph.shape):
+            raise RuntimeError(f"target heatmaps {tuple(gh.shape)} do not match the predicted {tuple(ph.shape)} "
+                               "(the reference's mse_loss fails the same way)")
+        pv = outputs["visibilities"]
+        if pv.dim() == 5:
+            pv = pv.squeeze(2)
+        if pv.dim() == 4:
+            pv = pv.max(dim=1)[0]
+        elif pv.dim() == 3 and pv.size(-1) != 3:
+            v3 = torch.zeros(pv.size(0), pv.size(2), 3, device=pv.device)
+            v3[:, :, 2] = pv.max(dim=1)[0]
+            pv = v3
+        gv = batch["visibilities"]
+        if gv.dim() == 3:
+            gv = gv.max(dim=1)[0]
+        pk = outputs["keypoints"]
+        if pk.dim() == 5:
+            pk = pk.squeeze(2)
+        loss, parts = self.loss_fn(predictions={"heatmaps": ph, "visibilities": pv, "keypoints": pk},
+                                   targets={"heatmaps": gh, "visibility": gv, "keypoints": batch["keypoints"]})
+        outputs["loss"] = loss
+        outputs.update(parts)
+        return outputs
+
+    def _forward(self, batch) -> Dict[str, torch.Tensor]:
         x = batch["image"] if isinstance(batch, dict) else batch
         if not isinstance(x, torch.Tensor):
             raise TypeError("Input must be a tensor or a dict with 'image' key containing a tensor")
         if self.training:
             raise NotImplementedError("training mode (batch-statistics BatchNorm, dropout, the loss) is outside "
                                       "the accelerated inference path; call model.eval()")
-        if isinstance(batch, dict) and "keypoints" in batch and "visibilities" in batch:
-            raise NotImplementedError("a batch with 'keypoints' and 'visibilities' asks for the training loss "
-                                      "and metrics (reference keypoint_model.py:208-209), which are outside the "
-                                      "accelerated inference path; pass only 'image' and 'bboxes'")
         if not x.is_cuda:
             raise _native.KpdNativeError("MultiPersonKeypointModel runs on the HIP device only; "
                                          "move the model input to 'cuda'")

@@ -2,7 +2,10 @@
 HeatmapHead's 3x3 convolution -- nn.Conv2d(C, O, 3, padding=1), reference
 dll/models/heatmap_head.py:31-45,55-66 -- as an autograd Function whose
 forward and backward both run native (libkpd: kpd_conv3x3_forward /
-kpd_conv3x3_backward, exact fp32 MFMA products, deterministic sums).  The
+kpd_conv3x3_backward: fp32-accurate split f16 hi / lo MFMA products with fp32
+accumulation for the forward and dgrad at 56 x 56 with 64 | 256 channels and
+for every wgrad, exact fp32 products on the generic fallback; deterministic
+sums).  The
 reference gets these gradients from autograd in Trainer.train
 (dll/training/trainer.py:263,272).
 

@@ -37,7 +37,10 @@ def test_inference_only_guards():
     with torch.no_grad(), pytest.raises(NotImplementedError, match="training mode"):
         m({"image": x})
     m.eval()
-    with pytest.raises(NotImplementedError, match="loss"):
+    # a batch with targets takes the same device path (its loss is added after
+    # the native forward): a CPU input still fails loudly, before any loss
+    from dll import _native
+    with pytest.raises(_native.KpdNativeError, match="HIP device"):
         m({"image": x, "bboxes": torch.zeros(1, 1, 4), "keypoints": torch.zeros(1, 1, 17, 2),
            "visibilities": torch.zeros(1, 1, 17)})
     with pytest.raises(TypeError):

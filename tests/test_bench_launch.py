@@ -40,14 +40,15 @@ def test_bench_gpus2_launches_two_ranks():
     assert line["ms_per_step"] == max(line["rank_ms_per_step"])
     assert line["collated"]["keypoints"] == [12, 2, 1, 17, 2]
     assert line["collated"]["visibilities"] == [12, 2, 1, 17, 3]
-    assert line["collated_ok"] is True
+    assert line["collated_ok"] is True and line["collated_index_ok"] is True
+    assert line["rccl_ranks"] == 2
     cfg = line["configs"]
     assert sorted(cfg) == ["C4", "C5"]
     c4, c5 = cfg["C4"], cfg["C5"]
     for c in (c4, c5):
         assert c["n_gpus"] == 2 and c["global_batch"] == 6 and c["images_per_rank"] == 3
         assert len(c["rank_ms_per_step"]) == 2 and c["ms_per_step"] == max(c["rank_ms_per_step"])
-        assert c["collated_ok"] is True and c["collated_index_ok"] is True
+        assert c["collated_ok"] is True and c["collated_index_ok"] is True and c["rccl_ranks"] == 2
         assert c["collated"]["keypoints"] == [6, 5, 1, 17, 2]
         assert c["collated"]["kh_visibilities"] == [6, 5, 1, 17, 3]
     assert c4["collated"]["boxes"] == [6, 5, 4] and c4["collated"]["box_scores"] == [6, 5]
@@ -58,7 +59,7 @@ def test_bench_gpus1_single_process():
     r = _run(["--gpus", "1", "--cpu-standin", "--steps", "2", "--warmup", "0", "--batch", "4", "--cfg-batch", "2"])
     assert r.returncode == 0, r.stderr[-3000:]
     line = _line(r.stdout)
-    assert line["n_gpus"] == 1 and line["world"] == 1 and line["collated"] == {}
+    assert line["n_gpus"] == 1 and line["world"] == 1 and line["collated"] == {} and line["rccl_ranks"] is None
     assert sorted(line["configs"]) == ["C3", "C5"]
     assert all("collated" not in c for c in line["configs"].values())
 

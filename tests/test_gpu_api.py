@@ -218,6 +218,44 @@ def test_backbone_forward_four_levels(model_sd, precision):
         np.testing.assert_allclose(o.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("hw", [(256, 192), (200, 152)])
+def test_backbone_body_and_fpn_submodules(model_sd, hw):
+    """backbone.body(x) returns the feature extractor's OrderedDict of the four
+    taps and backbone.fpn(taps) the four levels (reference backbone.py:29-39,
+    253-264), each native on its own; the FPN also on taps the caller made
+    (the oracle's), and with a level size that is not a 2x multiple of the
+    next (nearest indexing as F.interpolate)."""
+    from dll.models.synthetic import synthetic_images
+    m = _model(model_sd)
+    H, W = hw
+    img = synthetic_images(2, 3, H, W, seed=21)
+    taps = m.backbone.body(img.to(DEV))
+    assert list(taps.keys()) == ["feat0", "feat1", "feat2", "feat3"]
+    ref_taps = O.mbv3_small_taps(img, model_sd)
+    for t, r in zip(taps.values(), ref_taps):
+        assert t.shape == r.shape
+        np.testing.assert_allclose(t.cpu().numpy(), r.numpy(), rtol=1e-4, atol=1e-4)
+    outs = m.backbone.fpn(list(taps.values()))
+    own = m.backbone.fpn([r.to(DEV) for r in ref_taps])
+    lats = O.fpn_laterals(ref_taps, model_sd)
+    for i in range(4):
+        ref = O.fpn_level(lats[i], model_sd, i)
+        assert outs[i].shape == ref.shape
+        np.testing.assert_allclose(outs[i].cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(own[i].cpu().numpy(), ref.numpy(), rtol=1e-5, atol=2e-5)
+    # odd level sizes: level 1 at 13 x 9 upsampled from 6 x 5 (not 2x)
+    g = torch.Generator().manual_seed(5)
+    odd = [torch.rand(1, c, h, w, generator=g) for c, (h, w) in zip((16, 24, 48, 576),
+                                                                     ((52, 36), (13, 9), (6, 5), (3, 2)))]
+    got = m.backbone.fpn([o.to(DEV) for o in odd])
+    lats = O.fpn_laterals(odd, model_sd)
+    for i in range(4):
+        np.testing.assert_allclose(got[i].cpu().numpy(), O.fpn_level(lats[i], model_sd, i).numpy(), rtol=1e-5,
+                                   atol=2e-5)
+    with pytest.raises(ValueError):
+        m.backbone.fpn(list(taps.values())[:3])
+
+
 def test_person_head_forward(model_sd):
     from dll.models import MultiPersonKeypointModel  # noqa: F401
     m = _model(model_sd)

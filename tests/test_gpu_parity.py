@@ -321,6 +321,32 @@ def test_nms_prefix_paths():
     ref = O.nms(b4, s4, 0.3, 600, stable=True)
     assert torch.equal(got, ref)
     assert (s4[got] == 0.4).any()
+    # the tie order is implementation-defined (the reference sorts with an
+    # unstable sort): whatever order the kernel picks, its kept set must be a
+    # valid greedy-NMS result
+    _assert_greedy_nms(b3, eq, 0.3, _native.nms(b3.to(DEV), eq.to(DEV), 0.3, 0).cpu(), complete=True)
+    _assert_greedy_nms(b4, s4, 0.3, got, complete=False)
+    _assert_greedy_nms(boxes, tied, 0.3, _native.nms(boxes.to(DEV), tied.to(DEV), 0.3, 0).cpu(), complete=True)
+
+
+def _assert_greedy_nms(boxes, scores, thr, keep, complete):
+    """keep is a greedy NMS result under SOME order of tied scores: scores
+    non-increasing along keep, no kept pair above the IoU threshold, and every
+    box not kept that ranks above the last kept score (every box when the run
+    was not cut by max_output) overlaps a kept box scored at or above it."""
+    ks = scores[keep]
+    assert bool((ks[1:] <= ks[:-1]).all())
+    iou = O.box_iou_cxcywh(boxes[keep], boxes[keep])
+    iou.fill_diagonal_(0)
+    assert float(iou.max()) <= thr
+    dropped = torch.ones(len(boxes), dtype=torch.bool)
+    dropped[keep] = False
+    if not complete:
+        dropped &= scores > ks[-1]
+    idx = dropped.nonzero().flatten()
+    if idx.numel():
+        cover = (O.box_iou_cxcywh(boxes[idx], boxes[keep]) > thr) & (ks[None, :] >= scores[idx][:, None])
+        assert bool(cover.any(dim=1).all())
 
 
 def _dual_model(precision="fp32"):

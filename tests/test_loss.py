@@ -120,3 +120,110 @@ def test_gpu_quantile_select_exact():
         _, _, thr = _native.adaptive_heatmap_loss(x.to(DEV), x.to(DEV), None, 50.0, 1.0, True, 0.0, False)
         want = torch.clamp(torch.quantile(x.flatten(), 0.9), 0.05, 0.3)
         assert float(thr) == float(want) == float(LO.adaptive_threshold(x)), n
+
+
+# ---------------------------------------------------------------------------
+# KeypointLoss (ImprovedKeypointLoss) and the eval forward with targets
+# (reference keypoint_model.py:208-209, 509-584; keypoint_loss.py:28-393),
+# against goldens of the reference's own _compute_loss_and_metrics over a
+# 13-call sequence (tests/golden/make_kploss_golden.py): the balancer adapts
+# its weights at call 10.  Tolerances: components 2e-6 (heatmap: device
+# double sums vs torch fp32; coordinate / visibility: the same torch ops on
+# another device), weights and total 1e-5.
+# ---------------------------------------------------------------------------
+from kploss_cases import SEQ, checksum, make_call  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def kg(golden_dir):
+    return np.load(golden_dir / "kploss.npz", allow_pickle=False)
+
+
+def _glue_inputs(outputs, batch):
+    """The person-axis reductions of _compute_loss_and_metrics (reference :513-568)."""
+    pv = outputs["visibilities"].squeeze(2).max(dim=1)[0]
+    gv = batch["visibilities"].max(dim=1)[0]
+    return outputs["keypoints"].squeeze(2), batch["keypoints"], pv, gv
+
+
+def test_kploss_small_terms_and_balancer_vs_reference_golden(kg):
+    """CPU: the coordinate and visibility terms and the balancer's weight
+    sequence (fed the golden components) reproduce the reference's."""
+    from dll.losses import DynamicLossBalancer, SpatialCoordinateLoss
+    from dll.configs import TrainingConfig
+    tc = TrainingConfig()
+    bal = DynamicLossBalancer({"heatmap": tc.lambda_keypoint, "coordinate": 5.0, "visibility": tc.lambda_visibility})
+    coord = SpatialCoordinateLoss()
+    for i in range(len(SEQ)):
+        outputs, batch = make_call(i)
+        assert checksum(outputs, batch) == pytest.approx(float(kg[f"{i}/in_sum"]), rel=1e-12)
+        pk, gk, pv, gv = _glue_inputs(outputs, batch)
+        assert float(coord(pk, gk, gv)) == pytest.approx(float(kg[f"{i}/coordinate_loss"]), rel=2e-6)
+        ce = torch.nn.functional.cross_entropy(pv.reshape(-1, 3), gv.reshape(-1).long())
+        assert float(ce) == pytest.approx(float(kg[f"{i}/visibility_loss"]), rel=2e-6)
+        w = bal.update_weights({k: float(kg[f"{i}/{k}_loss"]) for k in ("heatmap", "coordinate", "visibility")})
+        np.testing.assert_allclose([w["heatmap"], w["coordinate"], w["visibility"]], kg[f"{i}/weights"], rtol=1e-12)
+
+
+def test_kploss_bad_shape_raises_like_reference():
+    """[B,P,K] terms against the [B,K] mask: P must be 1 or B (reference :186-187)."""
+    from dll.losses import SpatialCoordinateLoss
+    g = torch.Generator().manual_seed(0)
+    pk, gk = torch.rand(2, 3, 17, 2, generator=g), torch.rand(2, 3, 17, 2, generator=g)
+    with pytest.raises(RuntimeError):
+        SpatialCoordinateLoss()(pk, gk, torch.ones(2, 17))
+
+
+def _loss_model(sd):
+    from dll.configs import ModelConfig, TrainingConfig
+    from dll.models import MultiPersonKeypointModel
+    cfg = ModelConfig()
+    cfg.heatmap_head.heatmap_size = (56, 56)
+    m = MultiPersonKeypointModel(cfg, TrainingConfig())
+    m.load_state_dict(sd)
+    return m.to(DEV).eval()
+
+
+@gpu
+def test_kploss_sequence_vs_reference_golden(kg, model_sd):
+    """_compute_loss_and_metrics with the device heatmap term, call by call."""
+    m = _loss_model(model_sd)
+    for i in range(len(SEQ)):
+        outputs, batch = make_call(i)
+        o = {k: v.to(DEV) for k, v in outputs.items()}
+        b = {k: v.to(DEV) for k, v in batch.items()}
+        res = m._compute_loss_and_metrics(o, b)
+        for k in ("heatmap_loss", "coordinate_loss", "visibility_loss"):
+            assert res[k] == pytest.approx(float(kg[f"{i}/{k}"]), rel=2e-6), (i, k)
+        assert res["keypoint_loss"] == res["heatmap_loss"]
+        w = res["loss_weights"]
+        np.testing.assert_allclose([w["heatmap"], w["coordinate"], w["visibility"]], kg[f"{i}/weights"], rtol=1e-5)
+        assert float(res["loss"]) == pytest.approx(float(kg[f"{i}/loss"]), rel=1e-5)
+        assert res["loss_metrics"].total_loss == pytest.approx(float(res["loss"]), rel=1e-6)
+
+
+@gpu
+def test_eval_forward_with_targets(model_sd):
+    """model(batch) with 'keypoints' / 'visibilities' / 'heatmaps' (the
+    trainer's validation call, trainer.py:331-334) returns the eval outputs
+    plus the loss of those outputs; without 'heatmaps' the zero targets of
+    heatmap_size are used."""
+    from dll.models.synthetic import synthetic_boxes, synthetic_images
+    m, ref = _loss_model(model_sd), _loss_model(model_sd)
+    img = synthetic_images(2, 3, 256, 192, seed=31).to(DEV)
+    boxes = synthetic_boxes(2, 1, seed=32).to(DEV)
+    g = torch.Generator().manual_seed(33)
+    tg = {"keypoints": torch.rand(2, 1, 17, 2, generator=g).to(DEV),
+          "visibilities": torch.randint(0, 3, (2, 1, 17), generator=g).to(DEV),
+          "heatmaps": torch.rand(2, 1, 17, 56, 56, generator=g).to(DEV)}
+    out = m({"image": img, "bboxes": boxes, **tg})
+    plain = ref({"image": img, "bboxes": boxes})
+    for k in ("heatmap", "keypoints", "visibilities"):
+        assert torch.equal(out[k], plain[k])
+    exp = ref._compute_loss_and_metrics(dict(plain), {"image": img, **tg})
+    assert float(out["loss"]) == float(exp["loss"])
+    for k in ("heatmap_loss", "coordinate_loss", "visibility_loss", "total_loss"):
+        assert out[k] == exp[k]
+    tg.pop("heatmaps")
+    out2 = m({"image": img, "bboxes": boxes, **tg})
+    assert out2["heatmap_loss"] > 0 and np.isfinite(float(out2["loss"]))
