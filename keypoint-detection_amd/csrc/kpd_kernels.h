@@ -180,6 +180,24 @@ struct FirArgs {
 size_t fir_lds_bytes(const FirArgs& a, int K, int S);
 int fir_pick_rows(FirArgs& a, int K, int S);   // sets a.TH; 0 when the layer does not fit
 hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st);
+// features.2 + features.3 (the two SE-less inverted residuals, 3x3 stride 2
+// then 3x3 stride 1 with the residual) in one launch on row tiles (fir23.hip)
+struct Fir23Args {
+  const float* x;                      // features.1 output NHWC [N][H1][W1][16]
+  int H1, W1;
+  const float *we2, *be2, *wd2, *bd2;  // features.2 expand [E2][16], [E2]; depthwise [9][E2], [E2]
+  const float *wp2, *bp2;              // features.2 project [32][E2], [32]
+  const float *we3, *be3, *wd3, *bd3;  // features.3 expand [E3][32], [E3]; depthwise [9][E3], [E3]
+  const float *wp3, *bp3;              // features.3 project [32][E3], [32]
+  int E2, E3;                          // padded expanded widths (multiples of 16)
+  int act2e, act2d, act3e, act3d;
+  float* out;                          // features.3 output NHWC [N][H2][W2][32]
+  int H2, W2;
+  int T;                               // features.3 rows per workgroup (fir23_pick_rows)
+  unsigned long long* stamps;          // diagnostic phase stamps [grid][8] (KPD_STAMPS), normally null
+};
+int fir23_pick_rows(Fir23Args& a);   // sets a.T; 0 when the shapes do not fit
+hipError_t launch_fir23(const Fir23Args& a, int N, hipStream_t st);
 // fused expand 1x1 + depthwise + channel means (body_kernels.hip, exdw_kernel)
 struct ExDwArgs {
   const float* x;        // NHWC [N][Hi][Wi][cin_p]

@@ -1460,6 +1460,36 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       x = w.o[i];
       continue;
     }
+    // features.2 + features.3 (3x3 stride 2, then 3x3 stride 1 with the
+    // residual; no SE) in one launch: fir23.hip
+    static const bool no_fir23 = kpd_diag_env("KPD_NO_FIR23") != nullptr;   // A/B switch
+    if (!no_fuse && !no_fir23 && i + 1 < 11) {
+      const DevBneck& b3 = p->bn[i + 1];
+      auto plain = [](const DevConv& c) { return c.k == 1 && !c.bf16; };
+      const bool f23 = bn.has_exp && !bn.cfg.se && bn.dw.k == 3 && bn.dw.s == 2 && inp == 16 && plain(bn.expand) &&
+                       plain(bn.project) && bn.expand.cin_p == 16 && bn.expand.cout_p == bn.dw.Cp &&
+                       bn.project.cin_p == bn.dw.Cp && bn.project.cout_p == 32 && b3.has_exp && !b3.cfg.se &&
+                       b3.dw.k == 3 && b3.dw.s == 1 && plain(b3.expand) && plain(b3.project) &&
+                       b3.expand.cin_p == 32 && b3.expand.cout_p == b3.dw.Cp && b3.project.cin_p == b3.dw.Cp &&
+                       b3.project.cout_p == 32 && b3.cfg.cin == b3.cfg.cout && bn.cfg.cout == b3.cfg.cin;
+      Fir23Args fa{};
+      fa.x = x; fa.H1 = hi; fa.W1 = wi;
+      fa.we2 = static_cast<const float*>(bn.expand.w); fa.be2 = bn.expand.b; fa.wd2 = bn.dw.w; fa.bd2 = bn.dw.b;
+      fa.wp2 = static_cast<const float*>(bn.project.w); fa.bp2 = bn.project.b;
+      fa.we3 = static_cast<const float*>(b3.expand.w); fa.be3 = b3.expand.b; fa.wd3 = b3.dw.w; fa.bd3 = b3.dw.b;
+      fa.wp3 = static_cast<const float*>(b3.project.w); fa.bp3 = b3.project.b;
+      fa.E2 = bn.dw.Cp; fa.E3 = b3.dw.Cp;
+      fa.act2e = bn.cfg.act; fa.act2d = bn.dw.act; fa.act3e = b3.cfg.act; fa.act3d = b3.dw.act;
+      fa.out = w.o[i + 1]; fa.H2 = ho; fa.W2 = wo;
+      if (f23 && d.h[i + 2] == ho && d.w[i + 2] == wo && fir23_pick_rows(fa)) {
+        fa.stamps = take_stamps("stamps_fir23_0", (size_t)((ho + fa.T - 1) / fa.T) * B);
+        HIP_TRY(launch_fir23(fa, B, st));
+        ++i;   // features.3 done too
+        x = w.o[i];
+        if (i + 1 == 3) taps[1] = x;
+        continue;
+      }
+    }
     if (!no_fuse && fir_on && !bn.cfg.se && bn.has_exp && bn.expand.cout_p == bn.dw.Cp &&
         bn.project.cin_p == bn.dw.Cp) {
       FirArgs fa{};

@@ -45,7 +45,7 @@ def main():
         for _ in range(4):
             m(batch)
     torch.cuda.synchronize()
-    names = [f"stamps_{k}_{i}" for i in range(11) for k in ("exdw", "seproj")] + ["stamps_latchain_0"] + [f"stamps_fir_{i}" for i in range(11)] + ["stamps_roi_0", "stamps_roikh_0"]
+    names = [f"stamps_{k}_{i}" for i in range(11) for k in ("exdw", "seproj")] + ["stamps_latchain_0", "stamps_fir23_0"] + [f"stamps_fir_{i}" for i in range(11)] + ["stamps_roi_0", "stamps_roikh_0"]
     for name in names:
         try:
             buf = plan.debug_buffer(name)
