@@ -266,11 +266,18 @@ __device__ __forceinline__ void se_fc(const float* mean, float* hid, int nimg, i
 //   * the expanded slice lives in LDS only, rows padded to CS + 4 floats so the
 //     depthwise's 16-byte reads of 4 column groups hit distinct banks;
 //   * channel means reduced in a fixed order (deterministic, batch-independent).
+// LDS row stride (floats) of the expanded slice: CS + 4 pads the depthwise's
+// 16-byte reads apart; for the 32-channel stride-1 slices (features.10 / 11)
+// 48, which a simulation of the ds_read_b128 lane groups (lanes {0-3, 12-15,
+// 20-27}, {4-11, 16-19, 28-31} and + 32, MI355X_MICROARCH.md) over the
+// kernel's item -> lane map shows conflict-free (36: 2.2-way average)
+__host__ __device__ constexpr int exdw_estr(int CS, int S) { return CS == 32 && S == 1 ? 48 : CS + 4; }
+
 template <int K, int S, int NTC, int XT, int KC>
 __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
-  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = CS + 4, DA = KC <= 3 ? 4 : 1;
+  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = exdw_estr(CS, S), DA = KC <= 3 ? 4 : 1;
   const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int PD = (K - 1) / 2;
   // row band (blockIdx.z of gridDim.z; no SE): output rows [oy0, oy1), from
@@ -1466,7 +1473,7 @@ size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   const int Pin = std::min(a.Hi, ((a.Ho + nb - 1) / nb - 1) * S + K) * a.Wi, Po = a.Ho * a.Wo;
   // the fc1 columns are filled by 1 KiB LDS-DMA pieces: round up to whole pieces
   const size_t w1f = a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
-  const size_t main = (size_t)Pin * (a.CS + 4) + (size_t)(K * K + 1) * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
+  const size_t main = (size_t)Pin * exdw_estr(a.CS, S) + (size_t)(K * K + 1) * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
   return 4 * main;
 }
 
