@@ -61,8 +61,12 @@ __device__ __forceinline__ f32x4 mfma_k16(const float4 a, const float4 b, f32x4 
 // fp32 rounding.
 constexpr int NW = 8;
 
-template <int NK1, int NK2, int NK3, int T3, int T1, bool SPLIT>
+// REUSE (SPLIT, lateral 1 in one load batch per wave): the max|tap1| scan's
+// registers are lateral 1's A operands (the same pixels, tiles wave + NW j,
+// in the same lane layout), so lateral 1 issues no tap1 loads of its own.
+template <int NK1, int NK2, int NK3, int T3, int T1, bool SPLIT, bool REUSE = false>
 __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainArgs p) {
+  static_assert(!REUSE || (SPLIT && T1 == 6), "tap1 registers reused as lateral 1's A: one 6-tile batch");
   extern __shared__ __attribute__((aligned(16))) float lsm[];
   const int P1 = p.h1 * p.w1, P2 = p.h2 * p.w2, P3 = p.h3 * p.w3;
   float* l3 = lsm;                      // [P3][16]
@@ -127,11 +131,15 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
         if (t < nt3 && pp < P3) red[(wave * P3 + pp) * LG + r16] = acc[t][e];
       }
   }
+  float4 v[6][NK1];   // REUSE: tap1 tiles wave + NW j, kept for lateral 1
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int k = 0; k < NK1; ++k) v[j][k] = make_float4(0.f, 0.f, 0.f, 0.f);   // (lanes past the map: no load)
   if (SPLIT) {
     // max |tap1| of the image over the real channels: wave w scans pixels w, w + NW, ...
     // (batches of 6 pixel rows per lane, loads issued together)
     for (int px0 = wave * 16 + r16; px0 < P1; px0 += 6 * NW * 16) {
-      float4 v[6][NK1];
 #pragma unroll
       for (int j = 0; j < 6; ++j)
 #pragma unroll
@@ -238,7 +246,8 @@ __global__ __launch_bounds__(NW * 64) void lateral_chain_kernel(const LatChainAr
       for (int j = 0; j < JB; ++j) {
         const int px = min((t0 + NW * j) * 16 + r16, P1 - 1);
 #pragma unroll
-        for (int k = 0; k < NK1; ++k) a[j][k] = *reinterpret_cast<const float4*>(t1 + (size_t)px * (NK1 * 16) + 16 * k);
+        for (int k = 0; k < NK1; ++k)
+          a[j][k] = REUSE ? v[j][k] : *reinterpret_cast<const float4*>(t1 + (size_t)px * (NK1 * 16) + 16 * k);
       }
 #pragma unroll
       for (int j = 0; j < JB; ++j) {
@@ -336,7 +345,14 @@ hipError_t launch_lateral_chain(const LatChainArgs& a, int B, hipStream_t st) {
   const dim3 grid((unsigned)((B + 7) / 8 * 8), 128 / LG), block(NW * 64);
   const size_t lds = lateral_chain_lds_bytes(a);
   const bool small = a.h3 * a.w3 <= 16 * 3;
-  if (a.lat1_split) {
+  // REUSE when lateral 1 is one 6-tile batch per wave (A/B: KPD_LC_NOREUSE=1 off)
+  static const bool noreuse = kpd_diag_env("KPD_LC_NOREUSE") != nullptr;
+  const bool reuse = !noreuse && (long)a.h1 * a.w1 <= 6 * NW * 16;
+  if (a.lat1_split && small && reuse) {
+    hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3, 6, true, true>), grid, block, lds, st, q);
+  } else if (a.lat1_split && reuse) {
+    hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8, 6, true, true>), grid, block, lds, st, q);
+  } else if (a.lat1_split) {
     if (small) hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 3, 6, true>), grid, block, lds, st, q);
     else hipLaunchKernelGGL((lateral_chain_kernel<2, 3, 36, 8, 6, true>), grid, block, lds, st, q);
   } else {

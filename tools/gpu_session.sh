@@ -2,7 +2,7 @@
 # GPU session on one MI355X box (run through gpurun), every GPU step under its
 # own limit, stop at the first failure.  STEPS (space-separated, default
 # "test smoke bench prof"); output under gpurun_out/$TAG (TAG default r05):
-#   test    pytest -m gpu (TESTS= overrides the selection, e.g. "-k nms")
+#   test    pytest -m gpu (TESTS= overrides the selection, e.g. "-k nms"; TESTS_K= a -k expression with spaces)
 #   smoke   __graft_entry__.smoke()
 #   bench   the driver's exact command: python3 bench.py --gpus 1 --steps 20 --warmup 5
 #   prof    rocprofv3 --kernel-trace --stats of the C2 driver command and of the
@@ -45,7 +45,7 @@ for S in $STEPS; do
   case $S in
   test)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-      -p no:cacheprovider ${TESTS:-} > "$OUT/pytest_gpu.log" 2>&1 \
+      -p no:cacheprovider ${TESTS:-} ${TESTS_K:+-k "$TESTS_K"} > "$OUT/pytest_gpu.log" 2>&1 \
       || { echo "pytest rc=$?"; tail -40 "$OUT/pytest_gpu.log"; exit 1; }
     tail -1 "$OUT/pytest_gpu.log" ;;
   smoke)
