@@ -124,6 +124,8 @@ def parse(argv=None):
     ap.add_argument("--precision", default="split", choices=["fp32", "split", "mixed"],
                     help="split = fp32-accurate (the reference's precision); mixed = bf16 heatmap convs")
     ap.add_argument("--secondary", default="mixed", help="second, labelled precision line at N=1 ('' = none)")
+    ap.add_argument("--no-exact-check", dest="exact_check", action="store_false",
+                    help="skip the exact-product fp32 cross-check object (N=1)")
     ap.add_argument("--cpu-sample", type=int, default=64, help="images in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -964,6 +966,26 @@ def main(argv=None):
                              "roofline": roofline(a.secondary, st2, fl, Bl, a.height, a.width, pmc, d2),
                              "stages_ms": {k: round(v, 4) for k, v in st2.items()}}
         del m2, p2
+    if world == 1 and a.exact_check and a.precision != "fp32":
+        # cross-check of the headline precision: the same batch through the exact-product fp32 mode
+        # (every conv on fp32-input MFMA), its throughput and its distance from the headline outputs
+        m3 = build("fp32")
+        with torch.no_grad():
+            for _ in range(3):
+                out3 = step(m3)
+        n3 = max(1, min(a.steps, 10))
+        el4, out3 = run_steps(n3, 0, lambda: step(m3), False)
+        line["exact_fp32"] = {
+            "precision": "fp32", "dtype_detail": dtypes["fp32"][1], "steps": n3,
+            "value": round(B * n3 / el4, 2), "ms_per_step": round(el4 / n3 * 1e3, 4),
+            "vs_headline": {
+                "max_abs_dkpt": float((out3["keypoints"] - out["keypoints"]).abs().max()),
+                "max_abs_dheat": float((out3["heatmap"] - out["heatmap"]).abs().max()),
+                "vis_flips": int((out3["visibilities"].argmax(-1) != out["visibilities"].argmax(-1)).sum()),
+                "keypoints_compared": int(out["keypoints"][..., 0].numel())},
+            "note": "same batch and weights as the headline; the headline's split products against exact fp32 "
+                    "products (tolerances of the parity tests: 1e-5 keypoints, 5e-5 heatmaps)"}
+        del m3
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         ci = host_cpu_info()
         S = min(a.cpu_sample, B)
