@@ -137,7 +137,7 @@ def parse(argv=None):
                     help="N=1: also time the same workload at this many sub-batch streams (labelled "
                          "'alt_streams'; 0 = skip); the headline stays single-stream so the roofline's launch "
                          "times describe the kernel alone")
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r05" / "pmc.json"),
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "r06" / "pmc.json"),
                     help="per-launch HBM traffic of the dominant kernel from a rocprofv3 --pmc run (entries are "
                          "stamped with the hash of the kernel sources they were measured on)")
     ap.add_argument("--configs", default="auto",

@@ -84,14 +84,14 @@ for S in $STEPS; do
     python3 tools/prof_stages.py "$P/c3" --precision split --skip 6 --take 20 --tag C3 --out "$P/stages_c3.json" > "$P/stages_c3.txt"
     python3 tools/prof_stages.py "$P/c5" --precision split --skip 12 --take 40 --tag C5 --out "$P/stages_c5.json" > "$P/stages_c5.txt"
     python3 - "$P" "$OUT/pmc.json" <<'PY'
-import json, sys
+import json, re, sys
 p, out = sys.argv[1], sys.argv[2]
 m = {}
 for f in ("stages_c2.json", "stages_c3.json", "stages_c5.json"):
     d = json.load(open(f"{p}/{f}"))
     m.setdefault("_meta", {})[f] = d["_meta"]
     for k, v in d.items():
-        if ":" in k:
+        if re.fullmatch(r"[a-z0-9_]+:(split|mixed|fp32)(@C[0-9])?", k):   # stage entries (not kernel names)
             m[k] = v
 json.dump(m, open(out, "w"), indent=1)
 for k, v in m.items():
