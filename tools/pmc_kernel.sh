@@ -8,7 +8,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${TAG:-r06}"; O="$R/gpurun_out/$TAG/pmck"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 5 --warmup 3 --no-cpu-baseline --configs none --secondary= --alt-streams 0"
+ARGS="--steps 5 --warmup 3 --no-cpu-baseline --configs none --secondary= --alt-streams 0 --no-exact-check"
 IFS=";" read -ra PG <<< "${PMC_SETS:-SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE}"
 i=0
 for G in "${PG[@]}"; do
