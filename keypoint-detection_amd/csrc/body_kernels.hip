@@ -273,11 +273,17 @@ __device__ __forceinline__ void se_fc(const float* mean, float* hid, int nimg, i
 // kernel's item -> lane map shows conflict-free (36: 2.2-way average)
 __host__ __device__ constexpr int exdw_estr(int CS, int S) { return CS == 32 && S == 1 ? 48 : CS + 4; }
 
-template <int K, int S, int NTC, int XT, int KC>
+// BL (the 576-channel blocks, features.10 / 11): the expand's B fragments come
+// from LDS (staged by LDS-DMA with the first round trip, rows cin_p + 8 floats
+// apart: conflict-free fragment reads) instead of 48 registers, and the fc1
+// partial reads its weight columns from L2 instead of an LDS copy, so that
+// five workgroups fit a CU (LDS <= 32 KB, VGPRs <= 96): the launch's 1,152
+// workgroups in one round instead of two
+template <int K, int S, int NTC, int XT, int KC, bool BL = false>
 __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
-  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = exdw_estr(CS, S), DA = KC <= 3 ? 4 : 1;
+  constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = exdw_estr(CS, S), DA = KC <= 3 ? 4 : 1, WBS = 16 * KC + 8;
   const int n = blockIdx.y, c0 = blockIdx.x * CS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int PD = (K - 1) / 2;
   // row band (blockIdx.z of gridDim.z; no SE): output rows [oy0, oy1), from
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   float* es = sm;                                  // [Pin][ESTR]
   float* wds = es + Pin * ESTR;                    // [K*K][CS] depthwise weights, then [CS] its bias
   float* ds = wds + (K * K + 1) * CS;              // [Po][CS] (pooled)
-  float* w1s = ds + (p.pooled ? Po * CS : 0);      // [sq][CS] (part)
+  float* w1s = ds + (p.pooled ? Po * CS : 0);      // [sq][CS] (part; BL: [CS][WBS] expand weights)
   const float* xg = p.x + ((size_t)n * p.Hi + iy_lo) * p.Wi * cin_p;
   stamp(p.stamps, 0);
   const int r = lane & 15, g = lane >> 4;
@@ -297,12 +303,25 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
   // one round trip for everything the expand needs: B fragments (all k
   // chunks, all N tiles) and the first DA M tiles' A fragments -> registers,
   // then the depthwise weights and the fc1 columns -> LDS
-  float4 bw[NTC][KC];
+  float4 bw[BL ? 1 : NTC][BL ? 1 : KC];
+  if constexpr (!BL) {
 #pragma unroll
-  for (int nt = 0; nt < NTC; ++nt)
+    for (int nt = 0; nt < NTC; ++nt)
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      bw[nt][kc] = *reinterpret_cast<const float4*>(p.we + (size_t)(c0 + nt * 16 + r) * cin_p + kc * 16 + g * 4);
+      for (int kc = 0; kc < KC; ++kc)
+        bw[nt][kc] = *reinterpret_cast<const float4*>(p.we + (size_t)(c0 + nt * 16 + r) * cin_p + kc * 16 + g * 4);
+  } else {
+    // the slice's expand weight rows by LDS-DMA: 16-byte piece e of [CS][WBS]
+    // is row e / (WBS / 4), column piece e % (WBS / 4) (the last two: padding)
+    const i32x4 rwe = make_rsrc(p.we + (size_t)c0 * cin_p, CS * cin_p * 4);
+    const unsigned wb_lds = lds_addr(w1s);
+    constexpr int NPR = WBS / 4, NPC = (CS * NPR + 63) / 64;
+    for (int i = wave; i < NPC; i += 4) {
+      const int e = i * 64 + lane, row = e / NPR, cp = e - row * NPR;
+      const unsigned voff = (row < CS && cp < 4 * KC) ? (unsigned)((row * cin_p + cp * 4) * 4) : 0x80000000u;
+      glds16(rwe, __builtin_amdgcn_readfirstlane(wb_lds + i * 1024), voff, 0);
+    }
+  }
   float be[NTC];   // expand bias, loaded with the first round trip
 #pragma unroll
   for (int nt = 0; nt < NTC; ++nt) be[nt] = p.be[c0 + nt * 16 + r];
@@ -329,7 +348,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
     // the fc1 columns by LDS-DMA (no registers; waited for after the expand):
     // 16-byte piece e of w1s = [sq][CS] is w1[j][c0 + 4 q], e = j * CQ + q,
     // padding channels (>= C) load zeros through the range check
-    if (p.part) {
+    if (!BL && p.part) {
       const i32x4 rw1 = make_rsrc(p.w1, p.sq * p.C * 4);
       const unsigned w1s_lds = lds_addr(w1s);
       const int npc = (p.sq * CQ + 63) / 64;   // wave-instructions (1 KiB each)
@@ -344,6 +363,10 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       const int i = tid + u * 256;
       if (i < (K * K + 1) * CQ) reinterpret_cast<float4*>(wds)[i] = v[u];
     }
+  }
+  if constexpr (BL) {   // the expand weights' DMA landed (every wave's pieces)
+    wait_vmcnt<0>();
+    __syncthreads();
   }
   stamp(p.stamps, 1);
   // expand: DA M tiles of A in flight per wave; a tile's slot is refilled
@@ -361,10 +384,12 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
           for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
             for (int nt = 0; nt < NTC; ++nt) {
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].x, bw[nt][kc].x, acc[nt], 0, 0, 0);
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].y, bw[nt][kc].y, acc[nt], 0, 0, 0);
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].z, bw[nt][kc].z, acc[nt], 0, 0, 0);
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].w, bw[nt][kc].w, acc[nt], 0, 0, 0);
+              const float4 b4 = BL ? *reinterpret_cast<const float4*>(w1s + (nt * 16 + r) * WBS + kc * 16 + g * 4)
+                                   : bw[BL ? 0 : nt][BL ? 0 : kc];
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].x, b4.x, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].y, b4.y, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].z, b4.z, acc[nt], 0, 0, 0);
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][kc].w, b4.w, acc[nt], 0, 0, 0);
             }
           load_a(t + DA, av[d]);
           // C layout: col = lane & 15 (channel), row = 4 * (lane >> 4) + i (pixel)
@@ -380,7 +405,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       }
     }
   }
-  if (p.part) wait_vmcnt<0>();   // the fc1-column DMA (issued at the start; long landed)
+  if (!BL && p.part) wait_vmcnt<0>();   // the fc1-column DMA (issued at the start; long landed)
   __syncthreads();
   stamp(p.stamps, 2);
   // depthwise from LDS, XT consecutive output columns per thread (input
@@ -449,8 +474,23 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
       const int nsl = gridDim.x;
       for (int j = tid; j < p.sq; j += 256) {
         float acc = 0.f;
+        if constexpr (BL) {   // the fc1 columns from L2 (padding channels: zero weights)
+          float4 w4[CQ];
 #pragma unroll
-        for (int c2 = 0; c2 < CS; ++c2) acc = fmaf(w1s[j * CS + c2], ds[c2], acc);
+          for (int q = 0; q < CQ; ++q)
+            w4[q] = c0 + 4 * q < p.C ? *reinterpret_cast<const float4*>(p.w1 + (size_t)j * p.C + c0 + 4 * q)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int q = 0; q < CQ; ++q) {
+            acc = fmaf(w4[q].x, ds[4 * q + 0], acc);
+            acc = fmaf(w4[q].y, ds[4 * q + 1], acc);
+            acc = fmaf(w4[q].z, ds[4 * q + 2], acc);
+            acc = fmaf(w4[q].w, ds[4 * q + 3], acc);
+          }
+        } else {
+#pragma unroll
+          for (int c2 = 0; c2 < CS; ++c2) acc = fmaf(w1s[j * CS + c2], ds[c2], acc);
+        }
         p.part[((size_t)n * nsl + blockIdx.x) * p.sq + j] = acc;
       }
     }
@@ -1467,12 +1507,20 @@ hipError_t launch_fir(const FirArgs& a, int N, int K, int S, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the BL variant of exdw_kernel: the 576-wide stride-1 SE blocks (32-channel
+// slices of a 96-channel input; KPD_EXDW_NOBL=1, diagnostic build: off)
+bool exdw_bl(const ExDwArgs& a, int K) {
+  static const bool off = kpd_diag_env("KPD_EXDW_NOBL") != nullptr;
+  return !off && K == 5 && a.Hi == a.Ho && a.CS == 32 && a.cin_p == 96 && a.pooled && a.part && a.nband <= 1;
+}
+
 size_t exdw_lds_bytes(const ExDwArgs& a, int K) {
   // a band's input rows: at most ceil(Ho / nband) output rows' worth
   const int nb = a.nband > 1 ? a.nband : 1, S = a.Hi > a.Ho ? 2 : 1;
   const int Pin = std::min(a.Hi, ((a.Ho + nb - 1) / nb - 1) * S + K) * a.Wi, Po = a.Ho * a.Wo;
   // the fc1 columns are filled by 1 KiB LDS-DMA pieces: round up to whole pieces
-  const size_t w1f = a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
+  const size_t w1f = exdw_bl(a, K) ? ((size_t)a.CS * (a.cin_p + 8) + 255) / 256 * 256
+                   : a.part ? ((size_t)a.sq * a.CS + 255) / 256 * 256 : 0;
   const size_t main = (size_t)Pin * exdw_estr(a.CS, S) + (size_t)(K * K + 1) * a.CS + (a.pooled ? (size_t)Po * a.CS : 0) + w1f;
   return 4 * main;
 }
@@ -1488,6 +1536,11 @@ hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(a.Ep / a.CS, N, a.nband > 1 ? a.nband : 1);
   const bool xt4 = a.Wo >= 12;
+  if (exdw_bl(a, K)) {
+    if (xt4) hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 4, 6, true>), grid, dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 2, 6, true>), grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
 #define EXDW_KC(KK, SS, NTC, XT)                                                                        \
   do {                                                                                                  \
     if (kc == 2) hipLaunchKernelGGL((exdw_kernel<KK, SS, NTC, XT, 2>), grid, dim3(256), lds, st, a);   \
