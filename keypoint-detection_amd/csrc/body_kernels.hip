@@ -279,8 +279,11 @@ __host__ __device__ constexpr int exdw_estr(int CS, int S) { return CS == 32 && 
 // partial reads its weight columns from L2 instead of an LDS copy, so that
 // five workgroups fit a CU (LDS <= 32 KB, VGPRs <= 96): the launch's 1,152
 // workgroups in one round instead of two
-template <int K, int S, int NTC, int XT, int KC, bool BL = false>
+// ACT >= 0: both activations that compile-time constant (the runtime switch
+// of kpd_act costs a branch tree per element), else p.act_e / p.act_d
+template <int K, int S, int NTC, int XT, int KC, bool BL = false, int ACT = -1>
 __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
+  const int act_e = ACT >= 0 ? ACT : p.act_e, act_d = ACT >= 0 ? ACT : p.act_d;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   // KC = cin_p / 16 k chunks; DA = M tiles whose A loads are in flight per wave
   constexpr int CS = 16 * NTC, CQ = CS / 4, ESTR = exdw_estr(CS, S), DA = KC <= 3 ? 4 : 1, WBS = 16 * KC + 8;
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int px = mt * 16 + g * 4 + i;
-              if (px < Pin) es[px * ESTR + nt * 16 + r] = kpd_act(acc[nt][i] + be[nt], p.act_e);
+              if (px < Pin) es[px * ESTR + nt * 16 + r] = kpd_act(acc[nt][i] + be[nt], act_e);
             }
         }
       }
@@ -444,8 +447,8 @@ __global__ __launch_bounds__(256) void exdw_kernel(const ExDwArgs p) {
     for (int o = 0; o < XT; ++o) {
       if (ox0 + o >= p.Wo) break;
       float4 v;
-      v.x = kpd_act(a[o].x + b.x, p.act_d); v.y = kpd_act(a[o].y + b.y, p.act_d);
-      v.z = kpd_act(a[o].z + b.z, p.act_d); v.w = kpd_act(a[o].w + b.w, p.act_d);
+      v.x = kpd_act(a[o].x + b.x, act_d); v.y = kpd_act(a[o].y + b.y, act_d);
+      v.z = kpd_act(a[o].z + b.z, act_d); v.w = kpd_act(a[o].w + b.w, act_d);
       const int op = oy * p.Wo + ox0 + o;
       *reinterpret_cast<float4*>(p.out + ((size_t)n * Po + op) * p.Ep + c0 + q * 4) = v;
       if (p.pooled) reinterpret_cast<float4*>(ds)[op * CQ + q] = v;
@@ -1536,9 +1539,29 @@ hipError_t launch_exdw(const ExDwArgs& a, int N, int K, int S, hipStream_t st) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 grid(a.Ep / a.CS, N, a.nband > 1 ? a.nband : 1);
   const bool xt4 = a.Wo >= 12;
+  // the coarse SE blocks (features.4..11) use hardswish for both: that
+  // instance compiled with the constant (KPD_EXDW_RTACT=1, diagnostic build: the runtime switch)
+  static const bool rtact = kpd_diag_env("KPD_EXDW_RTACT") != nullptr;
+  const bool hs = !rtact && a.act_e == ACT_HSWISH && a.act_d == ACT_HSWISH;
   if (exdw_bl(a, K)) {
-    if (xt4) hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 4, 6, true>), grid, dim3(256), lds, st, a);
+    if (hs && xt4) hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 4, 6, true, ACT_HSWISH>), grid, dim3(256), lds, st, a);
+    else if (hs) hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 2, 6, true, ACT_HSWISH>), grid, dim3(256), lds, st, a);
+    else if (xt4) hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 4, 6, true>), grid, dim3(256), lds, st, a);
     else hipLaunchKernelGGL((exdw_kernel<5, 1, 2, 2, 6, true>), grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
+  // the hardswish instances the model's blocks take: features.4 (5x5 s2, 16-channel slices of 32
+  // input channels), .5-.8 (5x5 s1, 16-channel slices, 48 input channels), .9 (5x5 s2, 32-channel slices)
+  if (hs && K == 5 && S == 2 && a.CS == 16 && kc == 2 && xt4) {
+    hipLaunchKernelGGL((exdw_kernel<5, 2, 1, 4, 2, false, ACT_HSWISH>), grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
+  if (hs && K == 5 && S == 1 && a.CS == 16 && kc == 3 && xt4) {
+    hipLaunchKernelGGL((exdw_kernel<5, 1, 1, 4, 3, false, ACT_HSWISH>), grid, dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
+  if (hs && K == 5 && S == 2 && a.CS == 32 && kc == 3 && !xt4) {
+    hipLaunchKernelGGL((exdw_kernel<5, 2, 2, 2, 3, false, ACT_HSWISH>), grid, dim3(256), lds, st, a);
     return hipGetLastError();
   }
 #define EXDW_KC(KK, SS, NTC, XT)                                                                        \
