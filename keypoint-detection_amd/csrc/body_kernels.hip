@@ -759,12 +759,13 @@ __global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, floa
 //     recomputes it: 16 x 8 x 2 MACs) and the project 1x1 with the excitation
 //     applied to its input, one pixel per thread.
 constexpr int kDwsTH = 4;   // output rows per dwsum workgroup
-template <int K, int S>
+template <int K, int S, int ACT = -1>   // ACT >= 0: the activation as a compile-time constant
 __global__ __launch_bounds__(256) void dwsum_kernel(const float* __restrict__ in, int Hi, int Wi,
-                                                    const float* __restrict__ w, const float* __restrict__ b, int act,
+                                                    const float* __restrict__ w, const float* __restrict__ b, int act_rt,
                                                     float* __restrict__ out, int Ho, int Wo,
                                                     float* __restrict__ part) {
   constexpr int C = 16, CQ = 4, XT = 4, P = (K - 1) / 2, NC = (XT - 1) * S + K;
+  const int act = ACT >= 0 ? ACT : act_rt;
   __shared__ float4 red[256];
   const int n = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
   const int wx = (Wo + XT - 1) / XT, units = kDwsTH * wx * CQ;
@@ -911,7 +912,9 @@ __global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict_
 // v_mfma_f32_16x16x4_f32 (exact products), k-step t of a 16-wide chunk takes
 // element t of each lane's 16-byte load (same permutation for A and B).
 constexpr int kPwKC = 6;   // 16-wide k chunks (cin_p <= 96)
+template <int ACT = -1>   // ACT >= 0: the activation as a compile-time constant (features.12: hardswish)
 __global__ __launch_bounds__(256) void pw_small_kernel(const ConvArgs a) {
+  const int act = ACT >= 0 ? ACT : a.act;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 64 + wave * 16, n0 = blockIdx.y * 64;
   const int nkc = a.cin_p / 16, M = a.M;
@@ -979,7 +982,7 @@ __global__ __launch_bounds__(256) void pw_small_kernel(const ConvArgs a) {
     float mr = 0.f;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const float v = kpd_act(acc[nt][i] + bias[nt], a.act) + resv[nt][i];
+      const float v = kpd_act(acc[nt][i] + bias[nt], act) + resv[nt][i];
       out[(size_t)m * a.out_cstride + n0 + nt * 16 + r] = v;
       mr = fmaxf(mr, fabsf(v));
     }
@@ -1643,7 +1646,9 @@ hipError_t launch_dwsum(const float* in, int N, int Hi, int Wi, const float* w, 
   if (kDwsTH * ((Wo + 3) / 4) * 4 > 256) return hipErrorInvalidValue;
   const dim3 grid((Ho + kDwsTH - 1) / kDwsTH, N);
   *ntiles = (int)grid.x;
-  if (k == 3 && s == 2) hipLaunchKernelGGL((dwsum_kernel<3, 2>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
+  if (k == 3 && s == 2 && act == ACT_RELU)   // features.1 of mobilenet_v3_small
+    hipLaunchKernelGGL((dwsum_kernel<3, 2, ACT_RELU>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
+  else if (k == 3 && s == 2) hipLaunchKernelGGL((dwsum_kernel<3, 2>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
   else if (k == 3 && s == 1) hipLaunchKernelGGL((dwsum_kernel<3, 1>), grid, dim3(256), 0, st, in, Hi, Wi, w, b, act, out, Ho, Wo, part);
   else return hipErrorInvalidValue;
   return hipGetLastError();
@@ -1671,7 +1676,8 @@ bool pw_small_ok(const ConvArgs& a) {
 hipError_t launch_pw_small(const ConvArgs& a, hipStream_t st) {
   if (!pw_small_ok(a)) return hipErrorInvalidValue;
   const dim3 grid((a.M + 63) / 64, a.cout_p / 64);
-  hipLaunchKernelGGL(pw_small_kernel, grid, dim3(256), 0, st, a);
+  if (a.act == ACT_HSWISH) hipLaunchKernelGGL(pw_small_kernel<ACT_HSWISH>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(pw_small_kernel<>, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
