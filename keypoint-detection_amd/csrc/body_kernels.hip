@@ -1606,10 +1606,12 @@ hipError_t launch_seproj(const SeProjArgs& a, int N, hipStream_t st) {
   if (a.Ep % 16 || a.NT % 16 || a.cout_p % a.NT || a.sq > 144 || a.C > a.Ep || a.C % 4 ||
       (size_t)a.nsl * a.sq > 6 * 256 * 4 || (a.nsl * a.sq) % 4)
     return hipErrorInvalidValue;
-  // the 192-pixel maps split their rows over two workgroups (384 instead of
-  // 192 workgroups at 64 images; each recomputes the cheap excitation)
-  static const int msplit_env = kpd_diag_env("KPD_SEPROJ_MSPLIT") ? atoi(kpd_diag_env("KPD_SEPROJ_MSPLIT")) : 2;
-  const int msplit = mt_all == 12 ? std::max(1, msplit_env) : 1;
+  // the 192-pixel maps split their rows over workgroups, each recomputing the
+  // excitation: with 48-column tiles (all of features.4..8's outputs) four
+  // groups of 48 rows (256 workgroups at 64 images, 4 excitations per image),
+  // with 16-column tiles two (384 workgroups, 6 excitations per image)
+  static const int msplit_env = kpd_diag_env("KPD_SEPROJ_MSPLIT") ? atoi(kpd_diag_env("KPD_SEPROJ_MSPLIT")) : 0;
+  const int msplit = mt_all == 12 ? (msplit_env > 0 ? msplit_env : (a.NT >= 48 ? 4 : 2)) : 1;
   const int mt = (mt_all + msplit - 1) / msplit;
   SeProjArgs b = a;
   // the 48-pixel maps (3 row tiles): eight waves split the project's K

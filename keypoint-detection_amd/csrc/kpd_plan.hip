@@ -1544,7 +1544,11 @@ static int forward_one(kpd_plan* p, int k, bool debug, const float* image, int B
       sa.b1 = bn.se.b1; sa.w2t = bn.se.w2; sa.b2 = bn.se.b2;
       sa.wp = static_cast<const float*>(bn.project.w); sa.bp = bn.project.b; sa.cout_p = bn.project.cout_p;
       static const int nt_env = kpd_diag_env("KPD_SEPROJ_NT") ? atoi(kpd_diag_env("KPD_SEPROJ_NT")) : 0;
-      sa.NT = nt_env > 0 ? nt_env : (sa.Po == 48 ? 32 : 16);
+      // 192-pixel maps: all 48 output channels per workgroup and the rows in
+      // four (launch_seproj), so an image's excitation is recomputed by 4
+      // workgroups instead of 6 (its fc2 weight columns are most of a
+      // workgroup's L2 reads): body -8..-12 us at C2 (same-box A/B)
+      sa.NT = nt_env > 0 ? nt_env : (sa.Po == 48 ? 32 : 48);
       if (sa.cout_p % sa.NT) sa.NT = 16;
       const bool res = bn.cfg.s == 1 && bn.cfg.cin == bn.cfg.cout;
       sa.res = res ? x : nullptr;
