@@ -533,6 +533,13 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
   const int m0 = blockIdx.z * MP, Pr = min(MP, Po - m0);
   const float* dbase = a.d + ((size_t)n * Po + m0) * Ep;
   const int nkc = Ep / 16, ncw = (nkc - wave + NWV - 1) / NWV;   // this wave's k chunks: wave + NWV t
+  // the excitation's biases with the first round trip (loaded behind its
+  // barriers they were two more dependent round trips)
+  const float b1v = a.sesc ? 0.f : a.b1[min(tid, a.sq - 1)];
+  constexpr int NB2 = 1024 / NTH;   // Ep <= 1024
+  float b2v[NB2];
+#pragma unroll
+  for (int u = 0; u < NB2; ++u) b2v[u] = a.sesc ? 0.f : a.b2[min(tid + u * NTH, a.C - 1)];
   float4 av[D][MT], bv[D][NTT];
   auto load_chunk = [&](int t, float4* a4, float4* b4) {
     if (t < ncw) {
@@ -570,10 +577,10 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
       }
     }
     __syncthreads();
-    for (int j = tid; j < a.sq; j += NTH) {
+    if (tid < a.sq) {   // (sq <= 144 <= NTH)
       float h = 0.f;
-      for (int s2 = 0; s2 < a.nsl; ++s2) h += red[s2 * a.sq + j];
-      hid[j] = fmaxf(h + a.b1[j], 0.f);
+      for (int s2 = 0; s2 < a.nsl; ++s2) h += red[s2 * a.sq + tid];
+      hid[tid] = fmaxf(h + b1v, 0.f);
     }
     __syncthreads();
     stamp(a.stamps, 1);
@@ -604,11 +611,14 @@ __global__ __launch_bounds__(NWV * 64) void seproj_kernel(const SeProjArgs a) {
         reinterpret_cast<float4*>(fsum + (size_t)gi * a.C)[q] = acc4;
       }
       __syncthreads();
-      for (int c = tid; c < Ep; c += NTH) {
+#pragma unroll
+      for (int u = 0; u < NB2; ++u) {
+        const int c = tid + u * NTH;
+        if (c >= Ep) break;
         float t = 0.f;
         if (c < a.C)
           for (int gi = 0; gi < ngrp; ++gi) t += fsum[(size_t)gi * a.C + c];
-        sS[c] = c < a.C ? kpd_hsigmoid(t + a.b2[c]) : 0.f;
+        sS[c] = c < a.C ? kpd_hsigmoid(t + b2v[u]) : 0.f;
       }
       __syncthreads();
     }
@@ -706,6 +716,9 @@ __global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, floa
   // work item: thread (q = channel quad of 16, grp = j group of 16)
   const int q = tid & 15, grp = tid >> 4, jper = (a.sq + 15) / 16, j0 = grp * jper, j1 = min(a.sq, j0 + jper);
   const bool qlive = c0 + q * 4 < a.C;
+  // the biases with the first round trip (behind the barriers they were two
+  // more dependent round trips)
+  const float b1v = a.b1[min(tid, a.sq - 1)], b2v = a.b2[min(c0 + tid, a.C - 1)];
   constexpr int JMAX = 9;   // sq <= 144
   float4 wv[JMAX];
 #pragma unroll
@@ -724,10 +737,10 @@ __global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, floa
     }
   }
   __syncthreads();
-  for (int j = tid; j < a.sq; j += 256) {
+  if (tid < a.sq) {   // (sq <= 144)
     float h = 0.f;
-    for (int s2 = 0; s2 < a.nsl; ++s2) h += spart[s2 * a.sq + j];
-    hid[j] = fmaxf(h + a.b1[j], 0.f);
+    for (int s2 = 0; s2 < a.nsl; ++s2) h += spart[s2 * a.sq + tid];
+    hid[tid] = fmaxf(h + b1v, 0.f);
   }
   __syncthreads();
   float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -745,7 +758,7 @@ __global__ __launch_bounds__(256) void se_excite_kernel(const SeProjArgs a, floa
     float t = 0.f;
 #pragma unroll
     for (int gi = 0; gi < 16; ++gi) t += fsum[gi * 64 + tid];
-    if (c < a.Ep) sesc[(size_t)n * a.Ep + c] = c < a.C ? kpd_hsigmoid(t + a.b2[c]) : 0.f;
+    if (c < a.Ep) sesc[(size_t)n * a.Ep + c] = c < a.C ? kpd_hsigmoid(t + b2v) : 0.f;
   }
 }
 
@@ -839,7 +852,7 @@ __global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict_
                                                         const float* __restrict__ wp, const float* __restrict__ bp,
                                                         float* __restrict__ out) {
   constexpr int C = 16;
-  __shared__ float mean[C], hid[16], sc[C], wps[C * C], bps[C];
+  __shared__ float mean[C], hid[16], sc[C], wps[C * C], bps[C], w1s[16 * C], w2s[16 * C], b1s[16], b2s[C];
   const int n = blockIdx.y, tid = threadIdx.x;
   const int px = blockIdx.x * 256 + tid;
   // this thread's pixel first (its latency overlaps the excitation)
@@ -860,8 +873,16 @@ __global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict_
     for (int u = 0; u < 4; ++u)
       if (tid + u * 256 < ntiles * C) sp[tid + u * 256] = t4[u];
   }
+  // every weight of the excitation and the projection in the same round trip
+  // (loaded lazily they were two more dependent round trips behind barriers)
   if (tid < C * C) wps[tid] = wp[tid];
   if (tid < C) bps[tid] = bp[tid];
+  if (tid < sq * C) {
+    w1s[tid] = w1[tid];
+    w2s[tid] = w2t[tid];
+  }
+  if (tid < sq) b1s[tid] = b1[tid];
+  if (tid < C) b2s[tid] = b2[tid];
   __syncthreads();
   if (tid < C) {
     float t = 0.f;
@@ -872,14 +893,14 @@ __global__ __launch_bounds__(256) void se16_proj_kernel(const float* __restrict_
   if (tid < sq) {
     float a = 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) a = fmaf(w1[tid * C + c], mean[c], a);
-    hid[tid] = fmaxf(a + b1[tid], 0.f);
+    for (int c = 0; c < C; ++c) a = fmaf(w1s[tid * C + c], mean[c], a);
+    hid[tid] = fmaxf(a + b1s[tid], 0.f);
   }
   __syncthreads();
   if (tid < C) {
     float a = 0.f;
-    for (int j = 0; j < sq; ++j) a = fmaf(w2t[j * C + tid], hid[j], a);
-    sc[tid] = kpd_hsigmoid(a + b2[tid]);
+    for (int j = 0; j < sq; ++j) a = fmaf(w2s[j * C + tid], hid[j], a);
+    sc[tid] = kpd_hsigmoid(a + b2s[tid]);
   }
   __syncthreads();
   if (!live) return;
