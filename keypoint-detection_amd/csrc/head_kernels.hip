@@ -308,15 +308,31 @@ __device__ __forceinline__ void roi_row_sample(const float* __restrict__ feat, i
       __syncthreads();
       if (iy == 0) stamp(1);
       for (int ix = 0; ix < gw; ++ix) {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
+        // a bin's sample column is the same for every channel: lane j < NB
+        // computes bin wave + 4 j's (sample_x) and the bins take theirs by lane
+        // broadcasts, instead of every lane repeating all 14 bins' arithmetic
+        int cxl = 0, cxh = 0, cin = 0;
+        float clx = 0.f, chx = 0.f;
+        if (lane < NB) {
           int xl, xh;
           float lx, hx;
           bool xin;
-          sample_x(wave + 4 * j, ix, xl, xh, lx, hx, xin);
+          sample_x(wave + 4 * lane, ix, xl, xh, lx, hx, xin);
+          cxl = (xl - xlo) * CO;
+          cxh = (xh - xlo) * CO;
+          clx = lx;
+          chx = hx;
+          cin = xin ? 1 : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int oxl = __builtin_amdgcn_readlane(cxl, j), oxh = __builtin_amdgcn_readlane(cxh, j);
+          const float lx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, clx), j));
+          const float hx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, chx), j));
+          const bool xin = __builtin_amdgcn_readlane(cin, j) != 0;
 #pragma unroll
           for (int q = 0; q < CW; ++q) {
-            const float v = hx * stage[(xl - xlo) * CO + lane + TOPK * q] + lx * stage[(xh - xlo) * CO + lane + TOPK * q];
+            const float v = hx * stage[oxl + lane + TOPK * q] + lx * stage[oxh + lane + TOPK * q];
             acc[j][q] += xin ? v : 0.f;
           }
         }
