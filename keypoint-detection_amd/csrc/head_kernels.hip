@@ -350,10 +350,12 @@ __device__ __forceinline__ void roi_row_sample(const float* __restrict__ feat, i
     int yl = (int)yy, yh;
     if (yl >= Hf - 1) { yh = yl = Hf - 1; yy = (float)yl; } else yh = yl + 1;
     const float ly = yy - (float)yl, hy = 1.f - ly;
-    // the bins in groups of NBG (CW 2: two groups of 7 -- 14 bins x 4 corners
-    // x 2 channels of gathers in flight cost ~110 VGPRs and halved the
-    // resident waves); each bin still sums its samples in (iy, ix) order
-    constexpr int NBG = CW == 2 ? NB / 2 : NB;
+    // the bins in groups of NBG; each bin still sums its samples in (iy, ix)
+    // order.  CW 2 (roi_kh_kernel): one bin at a time -- this direct-gather
+    // fallback only runs for maps wider than the stage (Wf > 100), and its
+    // gathers in flight set the kernel's register peak (168 VGPRs with
+    // spills at two groups of 7; 127 at one bin: four workgroups per CU)
+    constexpr int NBG = CW == 2 ? 1 : NB;
     for (int ix = 0; ix < gw; ++ix)
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += NBG) {
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const float* __restrict_
 // the arithmetic of kh_att2_kernel.
 constexpr int kKaRow = 528;   // LDS bytes per pixel of the attention operand: hi 256 | lo 256 | 16 pad
 constexpr int kRoiKhLds = 64 * kKaRow;   // (>= 56 x 512 output staging)
-__global__ __launch_bounds__(256, 3) void roi_kh_kernel(const float* __restrict__ feat, int Hf, int Wf,
+__global__ __launch_bounds__(256, 4) void roi_kh_kernel(const float* __restrict__ feat, int Hf, int Wf,
                                                      const int32_t* __restrict__ topk,
                                                      const float* __restrict__ boxes, int P,
                                                      float* __restrict__ roi, float* __restrict__ roi_stats,
